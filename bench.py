@@ -1,0 +1,199 @@
+#!/usr/bin/env python
+"""Benchmark: env-steps/sec of the gfx950 vec-env (BASELINE.json metric).
+
+Default workload (BASELINE config 2, one GPU): 65,536 envs per GPU, env i
+seeded 42 + global index, HIP bitboard step + action mask + in-kernel
+auto-reset, actions from the synthetic random policy (Philox, fused into the
+step kernel).  One "step" = one bb_step launch over the whole batch.
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: launched by torch.distributed.run, one rank per GPU; envs are
+     independent shards, no collective on the data path -> weak scaling)
+
+Prints ONE JSON line on rank 0.  `roofline` prices the step kernel against
+HBM with the algorithmic bytes of SURVEY.md 8(d) (194 B per env-step) over its
+average launch duration measured here with HIP events on the launch stream;
+`cpu_baseline` times the CPU port of the reference's 64-env vectorised path
+(oracle/bb_game.py, one core) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd")
+for p in (PKG, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+ALGO_BYTES_PER_ENV_STEP = 194  # 2x80 B state + 4 action + 24 mask + 4 reward + 1 term + 1 lines
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+POLICY_SEED = 0xB10C
+
+
+def cpu_baseline(seconds: float = 12.0) -> dict:
+    """Reference path on the host: 64 envs stepped sequentially by the CPU
+    port of src/environment/wrappers.py (cell loops like the reference), with
+    random legal actions.  Bounded to ~`seconds` of CPU work."""
+    import numpy as np
+
+    from oracle import bb_game as O
+
+    n = 64
+    vec = O.VecEnv(n, seed=42)
+    obs, _ = vec.reset()
+    rng = np.random.default_rng(0)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        masks = obs["action_mask"].astype(bool)
+        acts = np.array([rng.choice(np.nonzero(m)[0]) for m in masks])
+        obs, *_ = vec.step(acts)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {
+        "value": round(n * steps / el, 2),
+        "unit": "env-steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n} envs x {steps} vec steps ({n * steps} env-steps, {el:.1f}s), random legal actions, "
+                  "CPU port of wrappers.py/block_blast_env.py/engine.py (oracle/bb_game.py), 1 Python thread",
+    }
+
+
+def load_traffic(n_envs: int):
+    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC run
+    (profiles/pmc_step_kernel.json, written by tools/pmc_traffic.py), or None."""
+    p = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if int(d.get("n_envs", -1)) == n_envs:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from runtime.device_env import DeviceEnvBatch
+
+    n = args.envs
+    offset = rank * n
+    env = DeviceEnvBatch(n, seeds=[42 + offset + i for i in range(n)], device=dev, env_offset=offset)
+    env.reset()
+    mbits = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+    env.obs(mask_bits=mbits)
+    act = [torch.zeros(n, dtype=torch.int32, device=dev), torch.zeros(n, dtype=torch.int32, device=dev)]
+    env.random_actions(mbits, act[0], seed=POLICY_SEED, step=0)
+
+    step_idx = [0]
+
+    def one_step():
+        t = step_idx[0]
+        env.step(act[t & 1], next_action=act[(t + 1) & 1], policy_seed=POLICY_SEED, policy_step=t + 1)
+        step_idx[0] = t + 1
+
+    for _ in range(args.warmup):
+        one_step()
+
+    # per-launch HIP events on the launch stream (torch's current stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record()
+        one_step()
+        ev[k][1].record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kern_ms = float(t[0]), float(t[1])
+
+    # sanity: every sampled action was legal -> no -10 rewards in the last step
+    assert bool((env.reward != -10.0).all()), "random policy produced an illegal action"
+
+    total_env_steps = n * world * args.steps
+    value = total_env_steps / el
+    if rank == 0:
+        algo_bytes = ALGO_BYTES_PER_ENV_STEP * n
+        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = load_traffic(n)
+        out = {
+            "metric": "env-steps/sec (whole node) at 64k parallel envs, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: numpy-exact PCG64 piece streams (env i seed 42+i), Philox random legal-action policy",
+            "config": {
+                "workload": "BASELINE config 2: 65,536 envs per MI355X, HIP bitboard step + action mask + "
+                            "auto-reset, random policy (env throughput)",
+                "envs_per_gpu": n,
+                "global_envs": n * world,
+                "parallelism": f"env shards x{world} (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "kernel": "bb::step_kernel",
+                "kernel_avg_ms": round(kern_ms, 5),
+                "algo_bytes_per_launch": algo_bytes,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,421 @@
+// bb_capi.cpp -- the C-ABI of include/bbvec.h on top of the gfx950 kernels.
+//
+// Owns the per-env device state (one hipMalloc slab, SoA columns aligned to
+// 256 B), the piece tables and the numpy-exact seeding.  No compute happens on
+// the host: there is no CPU fallback; every entry point that computes launches
+// a HIP kernel and fails loudly when the device is unusable.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "bb_env_internal.h"
+
+using namespace bb;
+
+struct bb_env {
+  int n = 0;
+  int device = 0;
+  int autoreset = 1;
+  bb_reward_cfg cfg{};
+  EnvDev d{};
+  PieceRow* d_rows = nullptr;
+  uint8_t* d_dtab = nullptr;
+  void* slab = nullptr;
+  std::string err;
+};
+
+static thread_local std::string g_create_err;
+
+namespace {
+
+int fail(bb_env* e, int code, const std::string& msg) {
+  if (e) e->err = msg;
+  else g_create_err = msg;
+  return code;
+}
+
+int hip_fail(bb_env* e, hipError_t st, const char* what) {
+  return fail(e, BB_ERR_HIP, std::string(what) + ": " + hipGetErrorString(st));
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {}
+};
+
+template <typename T>
+void carve(char*& cur, T*& out, size_t count) {
+  out = reinterpret_cast<T*>(cur);
+  size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+  cur += bytes;
+}
+
+size_t slab_bytes(int n) {
+  size_t b = 0;
+  auto add = [&](size_t count, size_t sz) { b += (count * sz + 255) & ~size_t(255); };
+  add(n, 8);      // board
+  add(n, 4);      // hand
+  add(n, 8);      // score
+  add(n, 4);      // combo
+  add(n, 4);      // max_combo
+  add(n, 4);      // moves
+  add(n, 4);      // lines
+  add(n, 4);      // blocks
+  add(n, 2);      // prev
+  add(3 * (size_t)n, 8);  // mask
+  add(n, 8);      // rng_hi
+  add(n, 8);      // rng_lo
+  add(n, 4);      // rng_buf
+  add(n, 8);      // inc_hi
+  add(n, 8);      // inc_lo
+  add(n, 8);      // seed_hi
+  add(n, 8);      // seed_lo
+  add(n, 1);      // has_seed
+  add(kPieces, sizeof(PieceRow));
+  add(kPieces * kPieces, 1);
+  return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bb_abi_version(void) { return BB_ABI_VERSION; }
+
+const char* bb_last_error(const bb_env* env) { return env ? env->err.c_str() : g_create_err.c_str(); }
+
+int32_t bb_num_envs(const bb_env* env) { return env ? env->n : 0; }
+
+int bb_pcg64_seed(uint64_t seed, uint64_t out[4]) {
+  if (!out) return BB_ERR_ARG;
+  pcg64_seed_numpy(seed, out);
+  return BB_OK;
+}
+
+int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_t autoreset, bb_env** out) {
+  if (!out) return fail(nullptr, BB_ERR_ARG, "bb_create: out is NULL");
+  *out = nullptr;
+  if (num_envs <= 0) return fail(nullptr, BB_ERR_ARG, "bb_create: num_envs must be positive");
+  if (!cfg) return fail(nullptr, BB_ERR_ARG, "bb_create: reward config is NULL");
+  int ndev = 0;
+  hipError_t st = hipGetDeviceCount(&ndev);
+  if (st != hipSuccess || ndev <= 0)
+    return fail(nullptr, BB_ERR_HIP, "bb_create: no HIP device available (this library has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(nullptr, BB_ERR_ARG, "bb_create: device index out of range");
+  DeviceGuard g(device);
+  bb_env* e = new bb_env();
+  e->n = num_envs;
+  e->device = device;
+  e->autoreset = autoreset ? 1 : 0;
+  e->cfg = *cfg;
+  const size_t bytes = slab_bytes(num_envs);
+  st = hipMalloc(&e->slab, bytes);
+  if (st != hipSuccess) {
+    std::string m = std::string("bb_create: hipMalloc: ") + hipGetErrorString(st);
+    delete e;
+    return fail(nullptr, BB_ERR_HIP, m);
+  }
+  (void)hipMemset(e->slab, 0, bytes);
+  char* cur = static_cast<char*>(e->slab);
+  const size_t n = (size_t)num_envs;
+  EnvDev& d = e->d;
+  d.n = num_envs;
+  carve(cur, d.board, n);
+  carve(cur, d.hand, n);
+  carve(cur, d.score, n);
+  carve(cur, d.combo, n);
+  carve(cur, d.max_combo, n);
+  carve(cur, d.moves, n);
+  carve(cur, d.lines, n);
+  carve(cur, d.blocks, n);
+  carve(cur, d.prev, n);
+  carve(cur, d.mask, 3 * n);
+  carve(cur, d.rng_hi, n);
+  carve(cur, d.rng_lo, n);
+  carve(cur, d.rng_buf, n);
+  carve(cur, d.inc_hi, n);
+  carve(cur, d.inc_lo, n);
+  carve(cur, d.seed_hi, n);
+  carve(cur, d.seed_lo, n);
+  carve(cur, d.has_seed, n);
+  carve(cur, e->d_rows, kPieces);
+  carve(cur, e->d_dtab, kPieces * kPieces);
+  PieceRow rows[kPieces];
+  uint8_t dtab[kPieces * kPieces];
+  build_piece_tables(rows, dtab);
+  st = hipMemcpy(e->d_rows, rows, sizeof(rows), hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(e->d_dtab, dtab, sizeof(dtab), hipMemcpyHostToDevice);
+  if (st != hipSuccess) {
+    std::string m = std::string("bb_create: table upload: ") + hipGetErrorString(st);
+    (void)hipFree(e->slab);
+    delete e;
+    return fail(nullptr, BB_ERR_HIP, m);
+  }
+  *out = e;
+  return BB_OK;
+}
+
+void bb_destroy(bb_env* env) {
+  if (!env) return;
+  DeviceGuard g(env->device);
+  if (env->slab) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(env->slab);
+  }
+  delete env;
+}
+
+int bb_seed(bb_env* env, const uint64_t* h_seeds, const uint8_t* h_has_seed, const uint64_t* h_raw) {
+  if (!env) return BB_ERR_ARG;
+  if (!h_has_seed) return fail(env, BB_ERR_ARG, "bb_seed: has_seed is NULL");
+  const int n = env->n;
+  std::vector<uint64_t> shi(n), slo(n), ihi(n), ilo(n);
+  std::vector<uint8_t> has(n);
+  for (int i = 0; i < n; ++i) {
+    uint64_t w[4];
+    if (h_has_seed[i] == 1) {
+      if (!h_seeds) return fail(env, BB_ERR_ARG, "bb_seed: seeds is NULL");
+      pcg64_seed_numpy(h_seeds[i], w);
+    } else {
+      if (!h_raw) return fail(env, BB_ERR_ARG, "bb_seed: raw state is NULL");
+      for (int k = 0; k < 4; ++k) w[k] = h_raw[4 * (size_t)i + k];
+      w[3] |= 1ull;  // PCG increments are odd
+    }
+    has[i] = h_has_seed[i] ? 1 : 0;
+    shi[i] = w[0];
+    slo[i] = w[1];
+    ihi[i] = w[2];
+    ilo[i] = w[3];
+  }
+  DeviceGuard g(env->device);
+  hipError_t st = hipDeviceSynchronize();
+  const size_t b8 = (size_t)n * 8;
+  if (st == hipSuccess) st = hipMemcpy(env->d.seed_hi, shi.data(), b8, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(env->d.seed_lo, slo.data(), b8, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(env->d.rng_hi, shi.data(), b8, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(env->d.rng_lo, slo.data(), b8, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(env->d.inc_hi, ihi.data(), b8, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(env->d.inc_lo, ilo.data(), b8, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(env->d.has_seed, has.data(), (size_t)n, hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemset(env->d.rng_buf, 0, (size_t)n * 4);
+  // clear has_uint32 in the hand words
+  if (st == hipSuccess) st = hipMemset(env->d.hand, 0, (size_t)n * 4);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_seed");
+  return BB_OK;
+}
+
+int bb_reset(bb_env* env, const uint8_t* d_env_mask, void* stream) {
+  if (!env) return BB_ERR_ARG;
+  DeviceGuard g(env->device);
+  hipError_t st = launch_reset(env->d, env->d_rows, env->d_dtab, d_env_mask, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_reset");
+  return BB_OK;
+}
+
+int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void* stream) {
+  if (!env) return BB_ERR_ARG;
+  if (!d_actions || !out || !out->reward || !out->terminated)
+    return fail(env, BB_ERR_ARG, "bb_step: actions, reward and terminated are required");
+  StepArgs a;
+  a.cfg = env->cfg;
+  a.center_tenth = env->cfg.center_bonus * 0.1;
+  a.autoreset = env->autoreset;
+  a.reward = out->reward;
+  a.terminated = out->terminated;
+  a.reward_f64 = out->reward_f64;
+  a.mask_out = out->mask;
+  a.lines = out->lines;
+  a.info = out->info;
+  a.next_action = out->next_action;
+  a.policy_seed = out->policy_seed;
+  a.policy_step = out->policy_step;
+  a.env_offset = out->env_offset;
+  DeviceGuard g(env->device);
+  hipError_t st = launch_step(env->d, env->d_rows, env->d_dtab, d_actions, a, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_step");
+  return BB_OK;
+}
+
+int bb_obs(bb_env* env, float* d_x, int8_t* d_mask_i8, float* d_mask_f32, uint64_t* d_mask_bits, void* stream) {
+  if (!env) return BB_ERR_ARG;
+  DeviceGuard g(env->device);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t st = launch_expand(env->d.board, env->d.hand, env->d.mask, nullptr, env->d_rows, env->n, d_x,
+                                d_mask_f32, d_mask_i8, s);
+  if (st == hipSuccess && d_mask_bits)
+    st = hipMemcpyAsync(d_mask_bits, env->d.mask, (size_t)env->n * 24, hipMemcpyDeviceToDevice, s);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_obs");
+  return BB_OK;
+}
+
+int bb_device_ptrs(bb_env* env, uint64_t** d_board, uint32_t** d_hand, uint64_t** d_mask) {
+  if (!env) return BB_ERR_ARG;
+  if (d_board) *d_board = env->d.board;
+  if (d_hand) *d_hand = env->d.hand;
+  if (d_mask) *d_mask = env->d.mask;
+  return BB_OK;
+}
+
+int bb_snapshot(bb_env* env, uint64_t* d_board, uint32_t* d_hand, uint64_t* d_mask_bits, void* stream) {
+  if (!env) return BB_ERR_ARG;
+  DeviceGuard g(env->device);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (size_t)env->n;
+  hipError_t st = hipSuccess;
+  if (d_board) st = hipMemcpyAsync(d_board, env->d.board, n * 8, hipMemcpyDeviceToDevice, s);
+  if (st == hipSuccess && d_hand) st = hipMemcpyAsync(d_hand, env->d.hand, n * 4, hipMemcpyDeviceToDevice, s);
+  if (st == hipSuccess && d_mask_bits)
+    st = hipMemcpyAsync(d_mask_bits, env->d.mask, n * 24, hipMemcpyDeviceToDevice, s);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_snapshot");
+  return BB_OK;
+}
+
+int bb_get_state(bb_env* env, const bb_state_view* v) {
+  if (!env || !v) return BB_ERR_ARG;
+  DeviceGuard g(env->device);
+  const size_t n = (size_t)env->n;
+  hipError_t st = hipDeviceSynchronize();
+  auto cp = [&](void* dst, const void* src, size_t bytes) {
+    if (dst && st == hipSuccess) st = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+  };
+  cp(v->board, env->d.board, n * 8);
+  cp(v->hand, env->d.hand, n * 4);
+  cp(v->score, env->d.score, n * 8);
+  cp(v->combo, env->d.combo, n * 4);
+  cp(v->max_combo, env->d.max_combo, n * 4);
+  cp(v->moves, env->d.moves, n * 4);
+  cp(v->lines, env->d.lines, n * 4);
+  cp(v->blocks, env->d.blocks, n * 4);
+  if ((v->prev_holes || v->prev_center) && st == hipSuccess) {
+    std::vector<uint16_t> prev(n);
+    st = hipMemcpy(prev.data(), env->d.prev, n * 2, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < n && st == hipSuccess; ++i) {
+      if (v->prev_holes) v->prev_holes[i] = (uint8_t)(prev[i] & 0xFF);
+      if (v->prev_center) v->prev_center[i] = (uint8_t)(prev[i] >> 8);
+    }
+  }
+  if (v->rng && st == hipSuccess) {
+    std::vector<uint64_t> hi(n), lo(n);
+    std::vector<uint32_t> buf(n);
+    st = hipMemcpy(hi.data(), env->d.rng_hi, n * 8, hipMemcpyDeviceToHost);
+    if (st == hipSuccess) st = hipMemcpy(lo.data(), env->d.rng_lo, n * 8, hipMemcpyDeviceToHost);
+    if (st == hipSuccess) st = hipMemcpy(buf.data(), env->d.rng_buf, n * 4, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < n && st == hipSuccess; ++i) {
+      v->rng[3 * i] = hi[i];
+      v->rng[3 * i + 1] = lo[i];
+      v->rng[3 * i + 2] = buf[i];
+    }
+  }
+  if (st != hipSuccess) return hip_fail(env, st, "bb_get_state");
+  return BB_OK;
+}
+
+int bb_set_state(bb_env* env, const bb_state_view* v) {
+  if (!env || !v) return BB_ERR_ARG;
+  DeviceGuard g(env->device);
+  const size_t n = (size_t)env->n;
+  hipError_t st = hipDeviceSynchronize();
+  auto cp = [&](void* dst, const void* src, size_t bytes) {
+    if (src && st == hipSuccess) st = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+  };
+  cp(env->d.board, v->board, n * 8);
+  cp(env->d.hand, v->hand, n * 4);
+  cp(env->d.score, v->score, n * 8);
+  cp(env->d.combo, v->combo, n * 4);
+  cp(env->d.max_combo, v->max_combo, n * 4);
+  cp(env->d.moves, v->moves, n * 4);
+  cp(env->d.lines, v->lines, n * 4);
+  cp(env->d.blocks, v->blocks, n * 4);
+  if ((v->prev_holes || v->prev_center) && st == hipSuccess) {
+    std::vector<uint16_t> prev(n);
+    st = hipMemcpy(prev.data(), env->d.prev, n * 2, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < n; ++i) {
+      uint16_t h = v->prev_holes ? v->prev_holes[i] : (uint16_t)(prev[i] & 0xFF);
+      uint16_t c = v->prev_center ? v->prev_center[i] : (uint16_t)(prev[i] >> 8);
+      prev[i] = (uint16_t)(h | (c << 8));
+    }
+    if (st == hipSuccess) st = hipMemcpy(env->d.prev, prev.data(), n * 2, hipMemcpyHostToDevice);
+  }
+  if (v->rng && st == hipSuccess) {
+    std::vector<uint64_t> hi(n), lo(n);
+    std::vector<uint32_t> buf(n);
+    for (size_t i = 0; i < n; ++i) {
+      hi[i] = v->rng[3 * i];
+      lo[i] = v->rng[3 * i + 1];
+      buf[i] = (uint32_t)v->rng[3 * i + 2];
+    }
+    st = hipMemcpy(env->d.rng_hi, hi.data(), n * 8, hipMemcpyHostToDevice);
+    if (st == hipSuccess) st = hipMemcpy(env->d.rng_lo, lo.data(), n * 8, hipMemcpyHostToDevice);
+    if (st == hipSuccess) st = hipMemcpy(env->d.rng_buf, buf.data(), n * 4, hipMemcpyHostToDevice);
+  }
+  // the mask column is derived state: recompute it from board + hand
+  if (st == hipSuccess && (v->board || v->hand)) {
+    st = launch_refresh_mask(env->d, env->d_rows, nullptr);
+    if (st == hipSuccess) st = hipDeviceSynchronize();
+  }
+  if (st != hipSuccess) return hip_fail(env, st, "bb_set_state");
+  return BB_OK;
+}
+
+int bb_random_actions(const uint64_t* d_mask_bits, int32_t n, uint64_t seed, uint64_t step, uint64_t env_offset,
+                      int32_t* d_actions, void* stream) {
+  if (!d_mask_bits || !d_actions || n < 0) return fail(nullptr, BB_ERR_ARG, "bb_random_actions: bad arguments");
+  hipError_t st = launch_random_actions(d_mask_bits, n, seed, step, env_offset, d_actions, (hipStream_t)stream);
+  if (st != hipSuccess) return fail(nullptr, BB_ERR_HIP, std::string("bb_random_actions: ") + hipGetErrorString(st));
+  return BB_OK;
+}
+
+int bb_masked_sample(const float* d_logits, const uint64_t* d_mask_bits, int32_t n, const float* d_uniform,
+                     uint64_t seed, uint64_t step, uint64_t env_offset, int32_t deterministic,
+                     const int64_t* d_action_in, int64_t* d_action, float* d_logp, float* d_entropy,
+                     void* stream) {
+  if (!d_logits || !d_mask_bits || n < 0) return fail(nullptr, BB_ERR_ARG, "bb_masked_sample: bad arguments");
+  if (n == 0) return BB_OK;
+  hipError_t st = launch_masked_sample(d_logits, d_mask_bits, n, d_uniform, seed, step, env_offset, deterministic,
+                                       d_action_in, d_action, d_logp, d_entropy, (hipStream_t)stream);
+  if (st != hipSuccess) return fail(nullptr, BB_ERR_HIP, std::string("bb_masked_sample: ") + hipGetErrorString(st));
+  return BB_OK;
+}
+
+int bb_gae(const float* d_rewards, const float* d_values, const float* d_dones, const float* d_last_values, int32_t T,
+           int32_t N, float gamma, float gamma_lambda, float* d_adv, float* d_ret, void* stream) {
+  if (!d_rewards || !d_values || !d_dones || !d_last_values || !d_adv || !d_ret || T <= 0 || N <= 0)
+    return fail(nullptr, BB_ERR_ARG, "bb_gae: bad arguments");
+  hipError_t st = launch_gae(d_rewards, d_values, d_dones, d_last_values, T, N, gamma, gamma_lambda, d_adv, d_ret,
+                             (hipStream_t)stream);
+  if (st != hipSuccess) return fail(nullptr, BB_ERR_HIP, std::string("bb_gae: ") + hipGetErrorString(st));
+  return BB_OK;
+}
+
+int bb_gather_obs(const uint64_t* d_board, const uint32_t* d_hand, const uint64_t* d_mask_bits,
+                  const int64_t* d_index, int32_t n, float* d_x, float* d_mask_f32, void* stream) {
+  if (n < 0 || (d_x && (!d_board || !d_hand)) || (d_mask_f32 && !d_mask_bits))
+    return fail(nullptr, BB_ERR_ARG, "bb_gather_obs: bad arguments");
+  if (n == 0) return BB_OK;
+  static PieceRow* s_rows = nullptr;  // per-process copy of the table for the stateless gather
+  static int s_dev = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!s_rows || s_dev != dev) {
+    PieceRow rows[kPieces];
+    uint8_t dtab[kPieces * kPieces];
+    build_piece_tables(rows, dtab);
+    hipError_t st = hipMalloc(&s_rows, sizeof(rows));
+    if (st == hipSuccess) st = hipMemcpy(s_rows, rows, sizeof(rows), hipMemcpyHostToDevice);
+    if (st != hipSuccess) return fail(nullptr, BB_ERR_HIP, std::string("bb_gather_obs: ") + hipGetErrorString(st));
+    s_dev = dev;
+  }
+  hipError_t st = launch_expand(d_board, d_hand, d_mask_bits, d_index, s_rows, n, d_x, d_mask_f32, nullptr,
+                                (hipStream_t)stream);
+  if (st != hipSuccess) return fail(nullptr, BB_ERR_HIP, std::string("bb_gather_obs: ") + hipGetErrorString(st));
+  return BB_OK;
+}
+
+}  // extern "C"

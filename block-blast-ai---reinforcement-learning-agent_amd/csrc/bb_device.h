@@ -1,0 +1,211 @@
+// bb_device.h -- device-side building blocks of the Block Blast vec-env (gfx950).
+//
+// Everything here works on one 8x8 board held as a uint64 bitboard in VGPRs
+// (bit r*8+c == grid[r][c], reference board.py:30).  Each helper names the
+// reference function whose semantics it reproduces.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bb {
+
+constexpr int kPieces = 37;
+constexpr int kHand = 3;
+constexpr int kMaxAttempts = 100;  // engine.py:161
+
+constexpr uint64_t kRow0 = 0x00000000000000FFull;
+constexpr uint64_t kRow7 = 0xFF00000000000000ull;
+constexpr uint64_t kCol0 = 0x0101010101010101ull;
+constexpr uint64_t kCol7 = 0x8080808080808080ull;
+constexpr uint64_t kCenter = 0x00003C3C3C3C0000ull;  // rows 2-5 x cols 2-5 (board.py:242)
+
+// One row of the piece table, staged into LDS by every kernel.
+//   shape   : cells of the piece anchored at (0,0)
+//   anchors : legal anchor squares on an empty board (r <= 8-h, c <= 8-w)
+//   offs    : 9 packed 6-bit cell offsets (padded by repetition) so that the
+//             blocked-anchor dilation is a fixed 9-step OR chain with no branch
+struct PieceRow {
+  uint64_t shape;
+  uint64_t anchors;
+  uint64_t offs;
+  uint32_t ncells;
+  uint32_t pad;
+};
+
+// Packed hand word (also the host-visible layout, see bbvec.h bb_state_view).
+__host__ __device__ inline uint32_t hand_id(uint32_t h, int slot) { return (h >> (6 * slot)) & 63u; }
+__host__ __device__ inline uint32_t hand_used(uint32_t h) { return (h >> 18) & 7u; }
+__host__ __device__ inline bool hand_over(uint32_t h) { return (h >> 21) & 1u; }
+__host__ __device__ inline bool hand_has32(uint32_t h) { return (h >> 22) & 1u; }
+__host__ __device__ inline uint32_t hand_pack(uint32_t a, uint32_t b, uint32_t c, uint32_t used,
+                                              bool over, bool has32) {
+  return a | (b << 6) | (c << 12) | (used << 18) | ((uint32_t)over << 21) | ((uint32_t)has32 << 22);
+}
+
+// --------------------------------------------------------------------------
+// Bitboard rules
+// --------------------------------------------------------------------------
+
+// Board.can_place over all anchors at once (board.py:71-93 x engine.py:364-380):
+// anchor a is blocked iff some cell a+off is filled, i.e. bit a of (B >> off).
+__device__ __forceinline__ uint64_t anchors_of(const PieceRow& p, uint64_t B) {
+  uint64_t acc = 0;
+  uint64_t offs = p.offs;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    acc |= B >> (offs & 63u);
+    offs >>= 6;
+  }
+  return p.anchors & ~acc;
+}
+
+// Board.find_complete_lines + clear_lines (board.py:144-193), and the DFS's
+// _simulate_line_clears (engine.py:226-238): full rows/cols are found on the
+// same board, then their union is cleared.
+__device__ __forceinline__ uint64_t clear_full(uint64_t B, int& rows, int& cols) {
+  uint64_t r = B & (B >> 1);
+  r &= r >> 2;
+  r &= r >> 4;
+  r &= kCol0;  // bit 8k set iff row k full
+  uint64_t c = B & (B >> 8);
+  c &= c >> 16;
+  c &= c >> 32;
+  c &= 0xFFull;  // bit k set iff column k full
+  rows = __popcll(r);
+  cols = __popcll(c);
+  uint64_t rm = (r << 8) - r;  // spread each row bit over its byte
+  uint64_t cm = c | (c << 8);
+  cm |= cm << 16;
+  cm |= cm << 32;
+  return B & ~(rm | cm);
+}
+
+__device__ __forceinline__ uint64_t clear_full(uint64_t B) {
+  int r, c;
+  return clear_full(B, r, c);
+}
+
+// Board.count_holes (board.py:195-216): empty cells whose four neighbours are
+// all filled or off-board.
+__device__ __forceinline__ int count_holes(uint64_t B) {
+  uint64_t n = (B << 8) | kRow0;
+  uint64_t s = (B >> 8) | kRow7;
+  uint64_t w = ((B << 1) & ~kCol0) | kCol0;
+  uint64_t e = ((B >> 1) & ~kCol7) | kCol7;
+  return __popcll(~B & n & s & w & e);
+}
+
+// --------------------------------------------------------------------------
+// numpy PCG64 (XSL-RR 128/64) + Generator.integers(0, 37) Lemire draw.
+// Stream-exact with np.random.default_rng (engine.py:109,138; pieces.py:354).
+// --------------------------------------------------------------------------
+struct Pcg {
+  uint64_t hi, lo;        // 128-bit LCG state
+  uint64_t inc_hi, inc_lo;
+  uint32_t buf;           // buffered upper 32-bit half (numpy `uinteger`)
+  bool has;               // numpy `has_uint32`
+};
+
+__device__ __forceinline__ uint64_t pcg_next64(Pcg& s) {
+  constexpr uint64_t MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
+  uint64_t lo = s.lo * ML;
+  uint64_t hi = __umul64hi(s.lo, ML) + s.lo * MH + s.hi * ML;
+  lo += s.inc_lo;
+  hi += s.inc_hi + (lo < s.inc_lo ? 1ull : 0ull);
+  s.lo = lo;
+  s.hi = hi;
+  uint64_t x = hi ^ lo;
+  unsigned rot = (unsigned)(hi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+__device__ __forceinline__ uint32_t pcg_next32(Pcg& s) {
+  if (s.has) {
+    s.has = false;
+    return s.buf;
+  }
+  uint64_t v = pcg_next64(s);
+  s.has = true;
+  s.buf = (uint32_t)(v >> 32);
+  return (uint32_t)v;
+}
+
+// buffered_bounded_lemire_uint32 with rng_excl = 37; threshold (2^32-37) % 37 = 7.
+__device__ __forceinline__ uint32_t draw_piece(Pcg& s) {
+  uint64_t m = (uint64_t)pcg_next32(s) * 37ull;
+  uint32_t left = (uint32_t)m;
+  if (left < 37u) {
+    while (left < 7u) {
+      m = (uint64_t)pcg_next32(s) * 37ull;
+      left = (uint32_t)m;
+    }
+  }
+  return (uint32_t)(m >> 32);
+}
+
+// --------------------------------------------------------------------------
+// Philox4x32-10 (Random123) -- synthetic policy / sampling uniforms.
+// --------------------------------------------------------------------------
+__host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += W0;
+      k1 += W1;
+    }
+    uint64_t p0 = (uint64_t)M0 * c[0];
+    uint64_t p1 = (uint64_t)M1 * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+  }
+}
+
+__device__ __forceinline__ void philox_words(uint64_t seed, uint64_t idx, uint64_t step, uint32_t out[4]) {
+  out[0] = (uint32_t)idx;
+  out[1] = (uint32_t)(idx >> 32);
+  out[2] = (uint32_t)step;
+  out[3] = (uint32_t)(step >> 32);
+  philox4x32_10(out, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// Index of the k-th (0-based) set bit of x (k < popcount(x)).
+__device__ __forceinline__ int select_bit(uint64_t x, uint32_t k) {
+  int pos = 0;
+  uint32_t c = __popc((uint32_t)x);
+  if (k >= c) { k -= c; x >>= 32; pos += 32; }
+  c = __popc((uint32_t)x & 0xFFFFu);
+  if (k >= c) { k -= c; x >>= 16; pos += 16; }
+  c = __popc((uint32_t)x & 0xFFu);
+  if (k >= c) { k -= c; x >>= 8; pos += 8; }
+  c = __popc((uint32_t)x & 0xFu);
+  if (k >= c) { k -= c; x >>= 4; pos += 4; }
+  c = __popc((uint32_t)x & 0x3u);
+  if (k >= c) { k -= c; x >>= 2; pos += 2; }
+  c = (uint32_t)x & 1u;
+  if (k >= c) { pos += 1; }
+  return pos;
+}
+
+// Synthetic random policy: the k-th legal action, k = (u * popcount) >> 32.
+__device__ __forceinline__ int32_t random_policy(uint64_t m0, uint64_t m1, uint64_t m2, uint64_t seed,
+                                                 uint64_t idx, uint64_t step) {
+  uint32_t w[4];
+  philox_words(seed, idx, step, w);
+  uint32_t c0 = __popcll(m0), c1 = __popcll(m1), c2 = __popcll(m2);
+  uint32_t tot = c0 + c1 + c2;
+  if (tot == 0) return 0;
+  uint32_t k = (uint32_t)(((uint64_t)w[0] * tot) >> 32);
+  if (k < c0) return select_bit(m0, k);
+  k -= c0;
+  if (k < c1) return 64 + select_bit(m1, k);
+  k -= c1;
+  return 128 + select_bit(m2, k);
+}
+
+}  // namespace bb

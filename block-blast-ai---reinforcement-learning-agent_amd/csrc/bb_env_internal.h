@@ -1,0 +1,71 @@
+// bb_env_internal.h -- device state layout shared by the kernels and the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bbvec.h"
+#include "bb_device.h"
+
+namespace bb {
+
+// Structure-of-arrays per-env state in HBM.
+// Hot columns (read+written every step): board, hand, score, combo,
+// max_combo, moves, lines, blocks, prev, mask.  PCG columns are touched only
+// on the steps that draw a hand (every third legal move) and on resets.
+struct EnvDev {
+  int n;
+  uint64_t* board;      // bitboard
+  uint32_t* hand;       // 3 x 6-bit ids | used<<18 | over<<21 | has_uint32<<22
+  int64_t* score;
+  int32_t* combo;
+  int32_t* max_combo;
+  int32_t* moves;
+  int32_t* lines;
+  int32_t* blocks;
+  uint16_t* prev;       // _prev_holes | filled-centre-cells << 8
+  uint64_t* mask;       // [n][3] current action-mask bits
+  uint64_t* rng_hi;     // PCG64 state
+  uint64_t* rng_lo;
+  uint32_t* rng_buf;    // buffered 32-bit half
+  uint64_t* inc_hi;     // PCG64 increment (constant per seed)
+  uint64_t* inc_lo;
+  uint64_t* seed_hi;    // state right after default_rng(seed_value)
+  uint64_t* seed_lo;
+  uint8_t* has_seed;    // seed_value is not None -> re-seed on reset
+};
+
+struct StepArgs {
+  bb_reward_cfg cfg;
+  double center_tenth;  // reward_config['center_bonus'] * 0.1 (block_blast_env.py:190)
+  int autoreset;
+  float* reward;
+  uint8_t* terminated;
+  double* reward_f64;
+  uint64_t* mask_out;
+  uint8_t* lines;
+  bb_info* info;
+  int32_t* next_action;
+  uint64_t policy_seed;
+  uint64_t policy_step;
+  uint64_t env_offset;
+};
+
+hipError_t launch_reset(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const uint8_t* sel, hipStream_t s);
+hipError_t launch_step(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const int32_t* actions,
+                       const StepArgs& a, hipStream_t s);
+hipError_t launch_expand(const uint64_t* board, const uint32_t* hand, const uint64_t* mbits, const int64_t* index,
+                         const PieceRow* rows, int n, float* x, float* mf, int8_t* mi, hipStream_t s);
+hipError_t launch_refresh_mask(const EnvDev& e, const PieceRow* rows, hipStream_t s);
+hipError_t launch_random_actions(const uint64_t* mbits, int n, uint64_t seed, uint64_t step, uint64_t offset,
+                                 int32_t* out, hipStream_t s);
+hipError_t launch_masked_sample(const float* logits, const uint64_t* mbits, int n, const float* uniform,
+                                uint64_t seed, uint64_t step, uint64_t offset, int deterministic,
+                                const int64_t* action_in, int64_t* action, float* logp, float* ent, hipStream_t s);
+hipError_t launch_gae(const float* r, const float* v, const float* d, const float* last, int T, int N, float gamma,
+                      float gl, float* adv, float* ret, hipStream_t s);
+
+// Host helpers (bb_tables.cpp).
+void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces]);
+void pcg64_seed_numpy(uint64_t seed, uint64_t out[4]);
+
+}  // namespace bb

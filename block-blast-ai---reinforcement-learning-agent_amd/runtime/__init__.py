@@ -1,0 +1,2 @@
+"""Native runtime: the ctypes boundary to libbbvec.so and device-side env handles."""
+from .lib import BBNativeError, load, check, pcg64_seed  # noqa: F401

@@ -1,0 +1,55 @@
+"""Build libbbvec.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+from .lib import LIB_PATH, PKG_DIR, REPO_DIR
+
+CSRC = os.path.join(PKG_DIR, "csrc")
+SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_capi.cpp", "bb_tables.cpp"]
+HEADERS = ["bb_device.h", "bb_solver.h", "bb_env_internal.h"]
+ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
+
+HIPCC_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-ffp-contract=off",  # reward / GAE arithmetic must not be fused into FMAs
+    "-fPIC",
+    "-shared",
+    "-Wno-unused-result",
+]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.isabs(cand) and os.path.exists(cand) or not os.path.isabs(cand)):
+            return cand
+    return "hipcc"
+
+
+def _stale(out: str, inputs) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(p) > t for p in inputs)
+
+
+def build_lib(force: bool = False, verbose: bool = True) -> str:
+    inputs = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(REPO_DIR, "include", "bbvec.h")]
+    if not force and not _stale(LIB_PATH, inputs):
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [_hipcc(), *HIPCC_FLAGS, f"-I{os.path.join(REPO_DIR, 'include')}",
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
+    if verbose:
+        print("[build]", " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build_lib(force="--force" in sys.argv)

@@ -1,0 +1,168 @@
+"""ctypes binding of ``include/bbvec.h`` (libbbvec.so, gfx950).
+
+This is the only way the product reaches its kernels.  There is no CPU
+fallback: if the library is missing or no HIP device is present, the first
+call raises ``BBNativeError`` with the reason.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.environ.get("BBVEC_LIB", os.path.join(PKG_DIR, "libbbvec.so"))
+
+BB_OK = 0
+BB_ACTIONS = 192
+BB_NUM_PIECES = 37
+
+
+class BBNativeError(RuntimeError):
+    """Raised when the HIP library is unavailable or a C-ABI call fails."""
+
+
+class RewardCfg(C.Structure):
+    _fields_ = [
+        ("line_clear_base", C.c_double),
+        ("block_placed", C.c_double),
+        ("game_over_penalty", C.c_double),
+        ("hole_penalty", C.c_double),
+        ("center_bonus", C.c_double),
+        ("combo_multiplier_bonus", C.c_double),
+        ("survival_bonus", C.c_double),
+    ]
+
+
+class Info(C.Structure):
+    _fields_ = [
+        ("score", C.c_int64),
+        ("score_gained", C.c_int64),
+        ("term_board", C.c_uint64),
+        ("moves", C.c_int32),
+        ("lines", C.c_int32),
+        ("max_combo", C.c_int32),
+        ("blocks", C.c_int32),
+        ("term_hand", C.c_uint32),
+        ("holes", C.c_uint8),
+        ("filled", C.c_uint8),
+        ("flags", C.c_uint8),
+        ("last_blocks", C.c_uint8),
+        ("last_lines", C.c_uint8),
+        ("last_cm", C.c_uint8),
+        ("pad", C.c_uint8 * 2),
+    ]
+
+
+INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
+
+
+class StepOut(C.Structure):
+    _fields_ = [
+        ("reward", C.c_void_p),
+        ("terminated", C.c_void_p),
+        ("reward_f64", C.c_void_p),
+        ("mask", C.c_void_p),
+        ("lines", C.c_void_p),
+        ("info", C.c_void_p),
+        ("next_action", C.c_void_p),
+        ("policy_seed", C.c_uint64),
+        ("policy_step", C.c_uint64),
+        ("env_offset", C.c_uint64),
+    ]
+
+
+class StateView(C.Structure):
+    _fields_ = [
+        ("board", C.c_void_p),
+        ("hand", C.c_void_p),
+        ("score", C.c_void_p),
+        ("combo", C.c_void_p),
+        ("max_combo", C.c_void_p),
+        ("moves", C.c_void_p),
+        ("lines", C.c_void_p),
+        ("blocks", C.c_void_p),
+        ("prev_holes", C.c_void_p),
+        ("prev_center", C.c_void_p),
+        ("rng", C.c_void_p),
+    ]
+
+
+_P = C.c_void_p
+_I32 = C.c_int32
+_U64 = C.c_uint64
+_F = C.c_float
+
+# name -> (restype, argtypes); exactly the entry points of include/bbvec.h
+SIGNATURES = {
+    "bb_abi_version": (C.c_int, []),
+    "bb_create": (C.c_int, [_I32, _I32, C.POINTER(RewardCfg), _I32, C.POINTER(_P)]),
+    "bb_destroy": (None, [_P]),
+    "bb_last_error": (C.c_char_p, [_P]),
+    "bb_num_envs": (_I32, [_P]),
+    "bb_pcg64_seed": (C.c_int, [_U64, C.POINTER(_U64)]),
+    "bb_seed": (C.c_int, [_P, _P, _P, _P]),
+    "bb_reset": (C.c_int, [_P, _P, _P]),
+    "bb_step": (C.c_int, [_P, _P, C.POINTER(StepOut), _P]),
+    "bb_obs": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "bb_device_ptrs": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P)]),
+    "bb_snapshot": (C.c_int, [_P, _P, _P, _P, _P]),
+    "bb_get_state": (C.c_int, [_P, C.POINTER(StateView)]),
+    "bb_set_state": (C.c_int, [_P, C.POINTER(StateView)]),
+    "bb_random_actions": (C.c_int, [_P, _I32, _U64, _U64, _U64, _P, _P]),
+    "bb_masked_sample": (C.c_int, [_P, _P, _I32, _P, _U64, _U64, _U64, _I32, _P, _P, _P, _P, _P]),
+    "bb_gae": (C.c_int, [_P, _P, _P, _P, _I32, _I32, _F, _F, _P, _P, _P]),
+    "bb_gather_obs": (C.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None):
+    """Load libbbvec.so (once) and bind every symbol of bbvec.h."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise BBNativeError(
+                f"HIP library not found at {p}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)"
+            )
+        lib = C.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)  # AttributeError == missing export
+            fn.restype = res
+            fn.argtypes = args
+        if lib.bb_abi_version() != 1:
+            raise BBNativeError("libbbvec ABI version mismatch")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def last_error(handle=None) -> str:
+    msg = load().bb_last_error(handle)
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str, handle=None) -> None:
+    if rc != BB_OK:
+        raise BBNativeError(f"{what} failed ({rc}): {last_error(handle)}")
+
+
+def pcg64_seed(seed: int):
+    """numpy-exact default_rng(seed) PCG64 words {state_hi, state_lo, inc_hi, inc_lo}."""
+    out = (_U64 * 4)()
+    check(load().bb_pcg64_seed(seed, out), "bb_pcg64_seed")
+    return [int(x) for x in out]
+
+
+def reward_cfg(rewards: dict) -> RewardCfg:
+    cfg = RewardCfg()
+    for name, _ in RewardCfg._fields_:
+        setattr(cfg, name, float(rewards[name]))
+    return cfg

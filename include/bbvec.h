@@ -1,0 +1,215 @@
+/*
+ * bbvec.h -- C-ABI of the MI355X-native Block Blast vectorised environment and
+ * masked-PPO rollout kernels (libbbvec.so, gfx950).
+ *
+ * This is the drop-in boundary under the reference's Python surface
+ * (SURVEY.md section 8(b)).  The reference has no FFI of its own; each entry
+ * point below names the reference interface it replaces, and INTEGRATION.md
+ * shows the ctypes binding a maintainer would add.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch types.  "d_" pointers are device
+ *     (HBM) pointers owned by the caller (e.g. tensor.data_ptr()); "h_" are host.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  All
+ *     launches are asynchronous on that stream; nothing allocates or syncs
+ *     inside bb_step / bb_obs / bb_masked_sample / bb_gae (graph-capturable).
+ *   - Return value: 0 = BB_OK, negative = error; bb_last_error() explains.
+ *     An invalid *action* is not an error: it is reproduced in-kernel as the
+ *     reference does (reward -10, no state change; block_blast_env.py:240-245).
+ *   - A handle is single-stream and not re-entrant (the reference is
+ *     single-threaded).  Multi-GPU = one handle per process/device.
+ *
+ * Mask bit layout (shared by every entry point): uint64 mask[N][3], word p is
+ * piece slot p, bit (r*8+c) set iff placing slot p at (r,c) is legal; flat
+ * action a = p*64 + r*8 + c (block_blast_env.py:104-132).
+ */
+#ifndef BBVEC_H
+#define BBVEC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BB_ABI_VERSION 1
+
+#define BB_OK 0
+#define BB_ERR_ARG (-1)
+#define BB_ERR_HIP (-2)
+#define BB_ERR_STATE (-3)
+
+#define BB_NUM_PIECES 37
+#define BB_ACTIONS 192
+
+typedef struct bb_env bb_env;
+
+/* Reward weights: block_blast_env.py:63-73 (defaults), overridable from the
+ * YAML `rewards:` section exactly like reward_config.update(). */
+typedef struct bb_reward_cfg {
+  double line_clear_base;        /* 1.0   */
+  double block_placed;           /* 0.01  */
+  double game_over_penalty;      /* -1.0  */
+  double hole_penalty;           /* -0.05 */
+  double center_bonus;           /* 0.02  */
+  double combo_multiplier_bonus; /* 0.5   */
+  double survival_bonus;         /* 0.001 */
+} bb_reward_cfg;
+
+/* Per-env info record written by bb_step (optional output).  Mirrors the
+ * `info` dict of block_blast_env.py:266-288 (values AFTER the move, BEFORE any
+ * auto-reset) plus the terminal-observation latch of wrappers.py:97-102. */
+typedef struct bb_info {
+  int64_t score;          /* info['score'] (== info['final_score'] on termination) */
+  int64_t score_gained;   /* info['last_move']['score_gained'] */
+  uint64_t term_board;    /* board bits before auto-reset (terminal_observation) */
+  int32_t moves;          /* info['moves'] */
+  int32_t lines;          /* info['lines_cleared'] (total) */
+  int32_t max_combo;      /* info['max_combo'] */
+  int32_t blocks;         /* info['blocks_placed'] (total) */
+  uint32_t term_hand;     /* packed hand word before auto-reset (see bb_state) */
+  uint8_t holes;          /* info['holes'] */
+  uint8_t filled;         /* popcount(board): info['board_fill'] = filled / 64 */
+  uint8_t flags;          /* bit0 invalid_action, bit1 terminated, bit2 has last_move */
+  uint8_t last_blocks;    /* info['last_move']['blocks_placed'] */
+  uint8_t last_lines;     /* info['last_move']['lines_cleared'] */
+  uint8_t last_cm;        /* info['last_move']['combo_multiplier'] */
+  uint8_t pad[2];
+} bb_info;
+
+/* Outputs of one bb_step.  reward and terminated are required, the rest may be
+ * NULL.  `next_action`, when non-NULL, runs the fused synthetic random policy
+ * (BASELINE config 2): for every env, u = Philox4x32-10(key=policy_seed,
+ * ctr=(env_offset+i, policy_step)).x, k = (u * popcount(mask)) >> 32, and the
+ * action is the k-th set bit of the post-step 192-bit mask (0 if empty). */
+typedef struct bb_step_out {
+  float* reward;          /* [N] f32 (wrappers.py:88,105)                       */
+  uint8_t* terminated;    /* [N] 0/1; truncated is always false                  */
+  double* reward_f64;     /* [N] optional: the fp64 reward BlockBlastEnv returns */
+  uint64_t* mask;         /* [N][3] optional: post-step (post-reset) mask bits   */
+  uint8_t* lines;         /* [N] optional: lines cleared by this move            */
+  bb_info* info;          /* [N] optional                                        */
+  int32_t* next_action;   /* [N] optional: fused random policy for the next step */
+  uint64_t policy_seed;
+  uint64_t policy_step;
+  uint64_t env_offset;    /* global index of env 0 (multi-GPU shards)            */
+} bb_step_out;
+
+/* Host view of the packed per-env state (bb_get_state / bb_set_state).
+ * hand word: bits 0-5 slot0 piece id, 6-11 slot1, 12-17 slot2, 18-20 used,
+ * 21 game_over, 22 pcg has_uint32.  Any pointer may be NULL (skipped). */
+typedef struct bb_state_view {
+  uint64_t* board;        /* [N] bit r*8+c = grid[r][c]                    */
+  uint32_t* hand;         /* [N] packed hand word                           */
+  int64_t* score;         /* [N]                                            */
+  int32_t* combo;         /* [N] combo_count (engine.py:115)                */
+  int32_t* max_combo;     /* [N]                                            */
+  int32_t* moves;         /* [N]                                            */
+  int32_t* lines;         /* [N] total_lines_cleared                        */
+  int32_t* blocks;        /* [N] total_blocks_placed                        */
+  uint8_t* prev_holes;    /* [N] BlockBlastEnv._prev_holes                  */
+  uint8_t* prev_center;   /* [N] filled centre cells behind _prev_center_openness */
+  uint64_t* rng;          /* [N][3] pcg state hi, state lo, uinteger        */
+} bb_state_view;
+
+/* ---- lifetime -------------------------------------------------------------
+ * bb_create replaces VectorizedBlockBlastEnv.__init__ (wrappers.py:21-51) /
+ * BlockBlastEnv.__init__ (block_blast_env.py:42-102).  autoreset=1 gives the
+ * vec-env semantics (wrappers.py:97-102), 0 the single-env semantics.  The new
+ * envs are unseeded until bb_seed + bb_reset. */
+int bb_abi_version(void);
+int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg,
+              int32_t autoreset, bb_env** out);
+void bb_destroy(bb_env* env);
+const char* bb_last_error(const bb_env* env); /* env may be NULL (last create error) */
+int32_t bb_num_envs(const bb_env* env);
+
+/* numpy-exact default_rng(seed) initialisation: SeedSequence(seed)
+ * .generate_state(4, uint64) -> PCG64 set_seed.  out = {state_hi, state_lo,
+ * inc_hi, inc_lo}.  Replaces np.random.default_rng (engine.py:109,138). */
+int bb_pcg64_seed(uint64_t seed, uint64_t out[4]);
+
+/* Per-env seeding (host arrays of length N).
+ *   has_seed[i] == 1: seeded from seeds[i] (numpy default_rng(seeds[i])) now
+ *     AND on every later reset -- the reference re-seeds each episode with
+ *     seed_value (block_blast_env.py:212-215, engine.py:137-138);
+ *   has_seed[i] == 2: same, but the post-seeding PCG64 words come from
+ *     raw[i*4..i*4+3] = {state_hi, state_lo, inc_hi, inc_lo} (seeds that do
+ *     not fit uint64, computed by the caller);
+ *   has_seed[i] == 0: raw words (e.g. fresh OS entropy) and the stream
+ *     continues across resets (seed_value None).
+ * raw may be NULL when every has_seed is 1. */
+int bb_seed(bb_env* env, const uint64_t* h_seeds, const uint8_t* h_has_seed,
+            const uint64_t* h_raw);
+
+/* Reset envs (all when d_env_mask is NULL, else those with mask[i] != 0):
+ * engine.py:127-153 + block_blast_env.py:195-222. */
+int bb_reset(bb_env* env, const uint8_t* d_env_mask, void* stream);
+
+/* One step of every env with actions d_actions[N] (int32 flat actions):
+ * VectorizedBlockBlastEnv.step (wrappers.py:75-116) -> BlockBlastEnv.step
+ * (block_blast_env.py:224-264) -> GameEngine.make_move (engine.py:390-454). */
+int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out,
+            void* stream);
+
+/* Observation expansion (engine.py:478-507, block_blast_env.py:134-146,
+ * wrappers.py:118-126).  Any output may be NULL:
+ *   d_x      [N][4][8][8] f32: plane 0 board, planes 1-3 unused piece shapes
+ *   d_mask_i8  [N][192] int8,  d_mask_f32 [N][192] f32,  d_mask_bits [N][3]. */
+int bb_obs(bb_env* env, float* d_x, int8_t* d_mask_i8, float* d_mask_f32,
+           uint64_t* d_mask_bits, void* stream);
+
+/* Device pointers of the live state columns (board [N], hand [N], mask
+ * [N][3]) for zero-copy snapshots into a device rollout buffer.  Valid until
+ * bb_destroy; read them on the stream that runs bb_step. */
+int bb_device_ptrs(bb_env* env, uint64_t** d_board, uint32_t** d_hand, uint64_t** d_mask);
+
+/* Async device-to-device snapshot of the packed observation state into caller
+ * buffers (the packed rollout-buffer record, ppo.py:100-102 without the f32
+ * planes): board [N] u64, hand [N] u32, mask [N][3] u64.  Any may be NULL. */
+int bb_snapshot(bb_env* env, uint64_t* d_board, uint32_t* d_hand, uint64_t* d_mask_bits, void* stream);
+
+/* Synchronous state copies (tests / info / checkpoint).  bb_set_state also
+ * overwrites the pcg state when v->rng is given. */
+int bb_get_state(bb_env* env, const bb_state_view* h_view);
+int bb_set_state(bb_env* env, const bb_state_view* h_view);
+
+/* Synthetic random policy on its own (see bb_step_out.next_action). */
+int bb_random_actions(const uint64_t* d_mask_bits, int32_t n, uint64_t seed,
+                      uint64_t step, uint64_t env_offset, int32_t* d_actions,
+                      void* stream);
+
+/* Fused masked-categorical tail of BlockBlastNetwork.get_action_and_value
+ * (network.py:173-180, 210-262; Categorical clamp semantics of torch 2.10):
+ * logits f32 [n][192] (raw policy-head output, unmasked) + mask bits ->
+ *   action (inverse-CDF sample with u from d_uniform[i] if non-NULL, else from
+ *   Philox(seed, (env_offset+i, step)) word 1; argmax when deterministic),
+ *   logp = log(clamp(p_a, 2^-23, 1-2^-23)), entropy = masked renormalised
+ *   entropy with 1e-10 clamps.  Any of action/logp/entropy may be NULL.
+ *   If d_action_in is non-NULL it is evaluated instead of sampling. */
+int bb_masked_sample(const float* d_logits, const uint64_t* d_mask_bits,
+                     int32_t n, const float* d_uniform, uint64_t seed,
+                     uint64_t step, uint64_t env_offset, int32_t deterministic,
+                     const int64_t* d_action_in, int64_t* d_action,
+                     float* d_logp, float* d_entropy, void* stream);
+
+/* GAE (RolloutBuffer.compute_returns_and_advantages, ppo.py:141-169) over
+ * [T][N] f32 arrays, numpy-2 float32 operation order, no FMA contraction.
+ * gamma and gamma_lambda are the f32 roundings of gamma and gamma*gae_lambda
+ * (the latter multiplied in double first, as Python does). */
+int bb_gae(const float* d_rewards, const float* d_values, const float* d_dones,
+           const float* d_last_values, int32_t T, int32_t N, float gamma,
+           float gamma_lambda, float* d_adv, float* d_ret, void* stream);
+
+/* Packed rollout-buffer record -> network input for a minibatch
+ * (RolloutBuffer.get_samples, ppo.py:171-213, with obs kept packed on device):
+ * for j < n, src = d_index[j]: x[j] = expand(board[src], hand[src]),
+ * mask_f32[j] = bits(mask[src]).  Either output may be NULL. */
+int bb_gather_obs(const uint64_t* d_board, const uint32_t* d_hand,
+                  const uint64_t* d_mask_bits, const int64_t* d_index,
+                  int32_t n, float* d_x, float* d_mask_f32, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BBVEC_H */
