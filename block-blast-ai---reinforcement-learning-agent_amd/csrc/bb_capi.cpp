@@ -6,6 +6,7 @@
 // a HIP kernel and fails loudly when the device is unusable.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -24,6 +25,9 @@ struct bb_env {
   PieceRow* d_rows = nullptr;
   uint8_t* d_dtab = nullptr;
   void* slab = nullptr;
+  int lane_budget = 0;  // 0: every hand search runs wave-cooperatively (escalate_kernel)
+  int dbg = 0;
+  uint64_t* dbg_out = nullptr;
   std::string err;
 };
 
@@ -78,6 +82,8 @@ size_t slab_bytes(int n) {
   add(n, 8);      // seed_hi
   add(n, 8);      // seed_lo
   add(n, 1);      // has_seed
+  add(n, 1);      // pend
+  add(n, 8);      // pscratch
   add(kPieces, sizeof(PieceRow));
   add(kPieces * kPieces, 1);
   return b;
@@ -115,6 +121,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   e->device = device;
   e->autoreset = autoreset ? 1 : 0;
   e->cfg = *cfg;
+  if (const char* s = getenv("BB_LANE_BUDGET")) e->lane_budget = atoi(s) > 0 ? atoi(s) : 0;
+  if (const char* s = getenv("BB_DEBUG_MODE")) e->dbg = atoi(s);
   const size_t bytes = slab_bytes(num_envs);
   st = hipMalloc(&e->slab, bytes);
   if (st != hipSuccess) {
@@ -145,6 +153,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   carve(cur, d.seed_hi, n);
   carve(cur, d.seed_lo, n);
   carve(cur, d.has_seed, n);
+  carve(cur, d.pend, n);
+  carve(cur, d.pscratch, n);
   carve(cur, e->d_rows, kPieces);
   carve(cur, e->d_dtab, kPieces * kPieces);
   PieceRow rows[kPieces];
@@ -158,6 +168,10 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
     delete e;
     return fail(nullptr, BB_ERR_HIP, m);
   }
+  if (e->dbg & 2) {
+    if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~2;
+    else (void)hipMemset(e->dbg_out, 0, n * 32);
+  }
   *out = e;
   return BB_OK;
 }
@@ -169,6 +183,7 @@ void bb_destroy(bb_env* env) {
     (void)hipDeviceSynchronize();
     (void)hipFree(env->slab);
   }
+  if (env->dbg_out) (void)hipFree(env->dbg_out);
   delete env;
 }
 
@@ -227,6 +242,9 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.cfg = env->cfg;
   a.center_tenth = env->cfg.center_bonus * 0.1;
   a.autoreset = env->autoreset;
+  a.lane_budget = env->lane_budget;
+  a.dbg = env->dbg;
+  a.dbg_out = env->dbg_out;
   a.reward = out->reward;
   a.terminated = out->terminated;
   a.reward_f64 = out->reward_f64;
@@ -361,6 +379,17 @@ int bb_set_state(bb_env* env, const bb_state_view* v) {
     if (st == hipSuccess) st = hipDeviceSynchronize();
   }
   if (st != hipSuccess) return hip_fail(env, st, "bb_set_state");
+  return BB_OK;
+}
+
+int bb_debug_counters(bb_env* env, uint64_t* h_out) {
+  if (!env || !h_out) return BB_ERR_ARG;
+  if (!env->dbg_out) return fail(env, BB_ERR_STATE, "bb_debug_counters: create with BB_DEBUG_MODE bit 1 set");
+  DeviceGuard g(env->device);
+  hipError_t st = hipDeviceSynchronize();
+  if (st == hipSuccess) st = hipMemcpy(h_out, env->dbg_out, (size_t)env->n * 32, hipMemcpyDeviceToHost);
+  if (st == hipSuccess) st = hipMemset(env->dbg_out, 0, (size_t)env->n * 32);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_debug_counters");
   return BB_OK;
 }
 

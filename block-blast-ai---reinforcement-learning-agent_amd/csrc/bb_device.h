@@ -24,10 +24,14 @@ constexpr uint64_t kCenter = 0x00003C3C3C3C0000ull;  // rows 2-5 x cols 2-5 (boa
 //   anchors : legal anchor squares on an empty board (r <= 8-h, c <= 8-w)
 //   offs    : 9 packed 6-bit cell offsets (padded by repetition) so that the
 //             blocked-anchor dilation is a fixed 9-step OR chain with no branch
+//   ym      : 128-bit "mirror" with bit (64 - o) for every cell offset o, the
+//             seed of the pair-conflict masks of bb_solver.h
 struct PieceRow {
   uint64_t shape;
   uint64_t anchors;
   uint64_t offs;
+  uint64_t ym_lo;
+  uint64_t ym_hi;
   uint32_t ncells;
   uint32_t pad;
 };

@@ -1,13 +1,24 @@
 // bb_env.hip -- MI355X (gfx950) vectorised Block Blast environment.
 //
-// One env per lane, wave64, 64-thread workgroups.  Per-env state lives in HBM
-// as structure-of-arrays (coalesced 4/8-byte columns); the 37-piece table and
-// the pair-offset table are staged into LDS once per workgroup.  A step reads
-// the state, applies the action on a uint64 bitboard, clears lines, scores,
-// draws a new hand when all three slots are used (numpy-exact PCG64 stream +
-// exact solvability test, hard boards escalated to the whole wave), computes
-// the shaped fp64 reward, the 192-bit action mask and the game-over flag,
-// auto-resets terminated envs, and writes state + outputs back.
+// One env per lane, wave64.  Per-env state lives in HBM as structure-of-arrays
+// (coalesced 2/4/8-byte columns); the 37-piece table and the pair-offset table
+// are staged into LDS once per workgroup.
+//
+// A step is two launches on one stream:
+//   step_kernel     -- every env: all state columns are loaded up front (one
+//                      memory round trip), the action is applied on a uint64
+//                      bitboard, lines cleared, scored; when all three slots are
+//                      used a new hand is drawn (numpy-exact PCG64 stream) and
+//                      tested for solvability under a per-lane work budget;
+//                      then reward (fp64, reference order), game over, info,
+//                      auto-reset, action mask and the fused random policy.
+//                      Envs whose hand search ran out of budget are parked:
+//                      post-move state + a pending flag.
+//   escalate_kernel -- each wave owns 16 envs; every parked env is finished by
+//                      its whole wave (lane-parallel over level-1 anchors) and
+//                      then finalised exactly like step_kernel would have.
+// Spreading the rare hard boards over 4x more waves than the step kernel
+// keeps the slowest wave short.
 //
 // Reference semantics: src/environment/wrappers.py:75-116 (vec step, auto-reset)
 // -> src/environment/block_blast_env.py:224-264 (step, invalid action, reward
@@ -15,15 +26,17 @@
 #include <hip/hip_runtime.h>
 
 #include "bb_device.h"
-#include "bb_solver.h"
 #include "bb_env_internal.h"
+#include "bb_solver.h"
 
 namespace bb {
 
-constexpr int kBlock = 64;
-// Per-lane search budget (anchors_of() evaluations) before a board is handed
-// to the whole wave.
-constexpr int kLaneBudget = 48;
+constexpr int kStepBlock = 64;
+constexpr int kEscBlock = 256;
+#ifndef BB_ESC_GROUP
+#define BB_ESC_GROUP 16
+#endif
+constexpr int kEscGroup = BB_ESC_GROUP;  // envs owned by one escalation wave
 
 struct Tables {
   PieceRow row[kPieces];
@@ -45,35 +58,48 @@ __device__ __forceinline__ void masks_of(const Tables& t, uint64_t B, uint32_t h
   }
 }
 
-__device__ __forceinline__ Pcg load_pcg(const EnvDev& e, int i, uint32_t hand) {
-  Pcg r;
-  r.hi = e.rng_hi[i];
-  r.lo = e.rng_lo[i];
-  r.inc_hi = e.inc_hi[i];
-  r.inc_lo = e.inc_lo[i];
-  r.buf = e.rng_buf[i];
-  r.has = hand_has32(hand);
-  return r;
+// Everything the finalisation of one env's step needs.
+struct StepCtx {
+  int i;
+  bool valid;
+  bool drew;
+  uint64_t B;
+  uint32_t hand;  // ids | used | has_uint32 (over bit set by finalize)
+  int64_t score;
+  int32_t combo, max_combo, moves, lines_tot, blocks;
+  uint32_t prev;
+  int nblk, lines, cm;
+  int64_t gained;
+  Pcg rng;  // inc always valid; state valid when drew (or loaded for reset)
+  uint64_t seed_hi, seed_lo;
+  bool has_seed;
+};
+
+// pending-record packing: attempt | nblk << 8 | lines << 16 | cm << 24 | gained << 32
+__device__ __forceinline__ uint64_t pack_pending(int attempt, int nblk, int lines, int cm, int64_t gained) {
+  return (uint64_t)attempt | ((uint64_t)nblk << 8) | ((uint64_t)lines << 16) | ((uint64_t)cm << 24) |
+         ((uint64_t)(uint32_t)gained << 32);
 }
 
 // ---------------------------------------------------------------------------
 // reset: engine.py:127-153 + block_blast_env.py:210-217
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void reset_lane(const Tables& t, const EnvDev& e, int i, Pcg& rng, uint64_t& B,
-                                           uint32_t& hand, uint64_t m[3]) {
-  if (e.has_seed[i]) {  // re-seed with seed_value every episode
-    rng.hi = e.seed_hi[i];
-    rng.lo = e.seed_lo[i];
+__device__ __forceinline__ void reset_lane(const Tables& t, bool has_seed, uint64_t seed_hi, uint64_t seed_lo,
+                                           Pcg& rng, uint64_t& B, uint32_t& hand, uint64_t m[3]) {
+  if (has_seed) {  // re-seed with seed_value every episode
+    rng.hi = seed_hi;
+    rng.lo = seed_lo;
     rng.buf = 0;
     rng.has = false;
   }
   B = 0;
-  uint32_t ids = 0;
-  int attempt = 0;
-  // On an empty board the first attempt always succeeds within a few anchor
-  // evaluations; the budget is unlimited so this never escalates.
-  gen_hand_lane(0ull, rng, ids, attempt, t.row, t.d, kUnlimited);
-  hand = hand_pack(ids & 63u, (ids >> 6) & 63u, (ids >> 12) & 63u, 0u, false, rng.has);
+  // Every one of the 37^3 hands fits an empty board (checked exhaustively
+  // against the reference DFS in tests/test_solver_bounds.py), so the first
+  // attempt of _generate_new_pieces always succeeds: three draws, no search.
+  const uint32_t a0 = draw_piece(rng);
+  const uint32_t a1 = draw_piece(rng);
+  const uint32_t a2 = draw_piece(rng);
+  hand = hand_pack(a0, a1, a2, 0u, false, rng.has);
   masks_of(t, B, hand, m);
 }
 
@@ -96,209 +122,85 @@ __device__ __forceinline__ void store_reset(const EnvDev& e, int i, const Pcg& r
   e.mask[3 * i + 2] = m[2];
 }
 
-__global__ void __launch_bounds__(kBlock) reset_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
-                                                       const uint8_t* sel) {
-  __shared__ Tables t;
-  stage_tables(t, g_rows, g_d);
-  const int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= e.n) return;
-  if (sel && !sel[i]) return;
-  Pcg rng = load_pcg(e, i, e.hand[i]);
-  uint64_t B;
-  uint32_t hand;
-  uint64_t m[3];
-  reset_lane(t, e, i, rng, B, hand, m);
-  store_reset(e, i, rng, hand, m);
-}
-
 // ---------------------------------------------------------------------------
-// step
+// finalize: game over, shaped reward, info, auto-reset, mask, policy, stores
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) step_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
-                                                      const int32_t* __restrict__ actions, StepArgs a) {
-  __shared__ Tables t;
-  stage_tables(t, g_rows, g_d);
-  const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * kBlock + threadIdx.x;
-  const bool live = i < e.n;
-
-  uint64_t B = 0;
-  uint32_t hand = 0;
-  int act = -1;
-  if (live) {
-    B = e.board[i];
-    hand = e.hand[i];
-    act = actions[i];
-  }
-
-  // ---- validity: block_blast_env.py:237-245 -> engine.py:326-346 ----------
-  const int p = act >> 6;           // a // 64 for a >= 0
-  const int cell = act & 63;        // r*8 + c
-  uint32_t used = hand_used(hand);
-  bool valid = live && act >= 0 && act < 192 && !hand_over(hand) && !((used >> p) & 1u);
-  PieceRow pr{};
-  if (valid) {
-    pr = t.row[hand_id(hand, p)];
-    valid = ((pr.anchors >> cell) & 1ull) && ((pr.shape << cell) & B) == 0;
-  }
-
-  // Running per-env state (only loaded when the move is legal).
-  Pcg rng{};
-  int64_t score = 0;
-  int combo = 0, max_combo = 0, moves = 0, lines_tot = 0, blocks = 0;
-  int nblk = 0, lines = 0, cm = 1;
-  int64_t gained = 0;
-  bool pending = false;
-  bool drew = false;
-  int attempt = 0;
-  uint32_t ids = hand & 0x3FFFFu;
-  uint32_t has_bit = hand & (1u << 22);
-  if (valid) {
-    score = e.score[i];
-    combo = e.combo[i];
-    max_combo = e.max_combo[i];
-    moves = e.moves[i];
-    lines_tot = e.lines[i];
-    blocks = e.blocks[i];
-    // ---- make_move: engine.py:406-429 ----------------------------------
-    nblk = (int)pr.ncells;
-    B |= pr.shape << cell;
-    used |= 1u << p;
-    moves += 1;
-    blocks += nblk;
-    int rows, cols;
-    B = clear_full(B, rows, cols);
-    lines = rows + cols;
-    if (lines > 0) {
-      combo += 1;
-      max_combo = combo > max_combo ? combo : max_combo;
-      lines_tot += lines;
-      cm = lines < 4 ? lines : 4;
-    } else {
-      combo = 0;
-    }
-    gained = nblk;
-    if (lines > 0) {
-      const int streak = combo + 1 < 8 ? combo + 1 : 8;  // post-increment combo (engine.py:261)
-      gained += (int64_t)(lines * 8 * 10) * cm * streak;  // blocks_in_lines = lines*8 (engine.py:427)
-    }
-    score += gained;
-    // ---- all three used -> new hand (engine.py:432-437) -----------------
-    if (used == 7u) {
-      rng = load_pcg(e, i, hand);
-      used = 0;
-      drew = true;
-      pending = !gen_hand_lane(B, rng, ids, attempt, t.row, t.d, kLaneBudget);
-    }
-  }
-
-  // ---- escalate budget-exhausted boards to the whole wave -----------------
-  uint64_t pend = __ballot(pending);
-  while (pend) {
-    const int src = __ffsll((unsigned long long)pend) - 1;
-    pend &= pend - 1;
-    Pcg w;
-    w.hi = __shfl(rng.hi, src);
-    w.lo = __shfl(rng.lo, src);
-    w.inc_hi = __shfl(rng.inc_hi, src);
-    w.inc_lo = __shfl(rng.inc_lo, src);
-    w.buf = __shfl(rng.buf, src);
-    w.has = __shfl((int)rng.has, src) != 0;
-    const uint64_t wB = __shfl(B, src);
-    const int watt = __shfl(attempt, src);
-    uint32_t wids = 0;
-    gen_hand_wave(wB, w, wids, watt, t.row, t.d, lane);
-    if (lane == src) {
-      rng = w;
-      ids = wids;
-    }
-  }
-
-  // ---- finalise: game over, reward, info, auto-reset, mask ---------------
-  if (!live) return;
+__device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepCtx& s, const StepArgs& a) {
+  const int i = s.i;
   uint64_t m[3];
-  if (valid) {
-    // numpy's has_uint32 flag lives in the hand word.
-    if (drew) has_bit = (uint32_t)rng.has << 22;
-    hand = (ids & 0x3FFFFu) | (used << 18) | has_bit;
-  }
-  masks_of(t, B, hand, m);
-
-  float rew32;
-  double rew = -10.0;
+  masks_of(t, s.B, s.hand, m);
+  double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
   bool term = false;
-  const uint32_t prev = valid ? (uint32_t)e.prev[i] : 0u;
-  int holes = 0;
-  int center = 0;
-  if (valid) {
+  int holes = 0, center = 0;
+  if (s.valid) {
     const bool over = (m[0] | m[1] | m[2]) == 0ull;  // engine.py:440-441
-    if (over) hand |= 1u << 21;
-    // ---- _calculate_reward: block_blast_env.py:158-193, fp64 in order -----
+    if (over) s.hand |= 1u << 21;
+    // _calculate_reward: block_blast_env.py:158-193, fp64 in this exact order
     double R = 0.0;
-    R = __dadd_rn(R, __dmul_rn((double)nblk, a.cfg.block_placed));
+    R = __dadd_rn(R, __dmul_rn((double)s.nblk, a.cfg.block_placed));
     R = __dadd_rn(R, a.cfg.survival_bonus);
-    if (lines > 0) {
-      double lr = __dmul_rn((double)lines, a.cfg.line_clear_base);
-      lr = __dmul_rn(lr, (double)cm);
+    if (s.lines > 0) {
+      double lr = __dmul_rn((double)s.lines, a.cfg.line_clear_base);
+      lr = __dmul_rn(lr, (double)s.cm);
       R = __dadd_rn(R, lr);
-      if (cm > 1) R = __dadd_rn(R, __dmul_rn((double)(cm - 1), a.cfg.combo_multiplier_bonus));
+      if (s.cm > 1) R = __dadd_rn(R, __dmul_rn((double)(s.cm - 1), a.cfg.combo_multiplier_bonus));
     }
     if (over) R = __dadd_rn(R, a.cfg.game_over_penalty);
-    holes = count_holes(B);
-    const int dh = holes - (int)(prev & 0xFFu);
+    holes = count_holes(s.B);
+    const int dh = holes - (int)(s.prev & 0xFFu);
     if (dh > 0) R = __dadd_rn(R, __dmul_rn((double)dh, a.cfg.hole_penalty));
-    center = __popcll(B & kCenter);
-    if (center <= (int)(prev >> 8)) R = __dadd_rn(R, a.center_tenth);  // openness >= previous
+    center = __popcll(s.B & kCenter);
+    if (center <= (int)(s.prev >> 8)) R = __dadd_rn(R, a.center_tenth);  // openness >= previous
     rew = R;
     term = over;
   } else if (a.info) {
-    holes = count_holes(B);
+    holes = count_holes(s.B);
   }
-  rew32 = (float)rew;
 
   if (a.info) {
     bb_info inf;
-    inf.score = valid ? score : e.score[i];
-    inf.score_gained = gained;
-    inf.term_board = B;
-    inf.moves = valid ? moves : e.moves[i];
-    inf.lines = valid ? lines_tot : e.lines[i];
-    inf.max_combo = valid ? max_combo : e.max_combo[i];
-    inf.blocks = valid ? blocks : e.blocks[i];
-    inf.term_hand = hand;
+    inf.score = s.score;
+    inf.score_gained = s.gained;
+    inf.term_board = s.B;
+    inf.moves = s.moves;
+    inf.lines = s.lines_tot;
+    inf.max_combo = s.max_combo;
+    inf.blocks = s.blocks;
+    inf.term_hand = s.hand;
     inf.holes = (uint8_t)holes;
-    inf.filled = (uint8_t)__popcll(B);
-    inf.flags = (uint8_t)((valid ? 0u : 1u) | (term ? 2u : 0u) | (valid ? 4u : 0u));
-    inf.last_blocks = (uint8_t)nblk;
-    inf.last_lines = (uint8_t)lines;
-    inf.last_cm = (uint8_t)cm;
+    inf.filled = (uint8_t)__popcll(s.B);
+    inf.flags = (uint8_t)((s.valid ? 4u : 1u) | (term ? 2u : 0u));
+    inf.last_blocks = (uint8_t)s.nblk;
+    inf.last_lines = (uint8_t)s.lines;
+    inf.last_cm = (uint8_t)s.cm;
     inf.pad[0] = inf.pad[1] = 0;
     a.info[i] = inf;
   }
-  a.reward[i] = rew32;
+  a.reward[i] = (float)rew;
   a.terminated[i] = term ? 1 : 0;
   if (a.reward_f64) a.reward_f64[i] = rew;
-  if (a.lines) a.lines[i] = (uint8_t)lines;
+  if (a.lines) a.lines[i] = (uint8_t)s.lines;
 
   if (term && a.autoreset) {
-    // wrappers.py:97-102: env.reset() with the stored seed_value.
-    if (!drew) rng = load_pcg(e, i, hand);  // unseeded envs continue their stream
-    reset_lane(t, e, i, rng, B, hand, m);
-    store_reset(e, i, rng, hand, m);
-  } else if (valid) {
-    e.board[i] = B;
-    e.hand[i] = hand;
-    if (drew) {
-      e.rng_hi[i] = rng.hi;
-      e.rng_lo[i] = rng.lo;
-      e.rng_buf[i] = rng.buf;
+    // wrappers.py:97-102: env.reset() with the stored seed_value
+    uint64_t B;
+    uint32_t hand;
+    reset_lane(t, s.has_seed, s.seed_hi, s.seed_lo, s.rng, B, hand, m);
+    store_reset(e, i, s.rng, hand, m);
+  } else if (s.valid) {
+    e.board[i] = s.B;
+    e.hand[i] = s.hand;
+    if (s.drew) {
+      e.rng_hi[i] = s.rng.hi;
+      e.rng_lo[i] = s.rng.lo;
+      e.rng_buf[i] = s.rng.buf;
     }
-    e.score[i] = score;
-    e.combo[i] = combo;
-    e.max_combo[i] = max_combo;
-    e.moves[i] = moves;
-    e.lines[i] = lines_tot;
-    e.blocks[i] = blocks;
+    e.score[i] = s.score;
+    e.combo[i] = s.combo;
+    e.max_combo[i] = s.max_combo;
+    e.moves[i] = s.moves;
+    e.lines[i] = s.lines_tot;
+    e.blocks[i] = s.blocks;
     e.prev[i] = (uint16_t)(holes | (center << 8));
     e.mask[3 * i + 0] = m[0];
     e.mask[3 * i + 1] = m[1];
@@ -311,6 +213,233 @@ __global__ void __launch_bounds__(kBlock) step_kernel(EnvDev e, const PieceRow* 
   }
   if (a.next_action) {
     a.next_action[i] = random_policy(m[0], m[1], m[2], a.policy_seed, a.env_offset + (uint64_t)i, a.policy_step);
+  }
+}
+
+__global__ void __launch_bounds__(kStepBlock) reset_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
+                                                           const uint8_t* sel) {
+  __shared__ Tables t;
+  stage_tables(t, g_rows, g_d);
+  const int i = blockIdx.x * kStepBlock + threadIdx.x;
+  if (i >= e.n) return;
+  if (sel && !sel[i]) return;
+  const uint32_t h0 = e.hand[i];
+  Pcg rng;
+  rng.hi = e.rng_hi[i];
+  rng.lo = e.rng_lo[i];
+  rng.inc_hi = e.inc_hi[i];
+  rng.inc_lo = e.inc_lo[i];
+  rng.buf = e.rng_buf[i];
+  rng.has = hand_has32(h0);
+  uint64_t B;
+  uint32_t hand;
+  uint64_t m[3];
+  reset_lane(t, e.has_seed[i] != 0, e.seed_hi[i], e.seed_lo[i], rng, B, hand, m);
+  store_reset(e, i, rng, hand, m);
+  e.pend[i] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// step
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
+                                                          const int32_t* __restrict__ actions, StepArgs a) {
+  __shared__ Tables t;
+  stage_tables(t, g_rows, g_d);
+  const int i = blockIdx.x * kStepBlock + threadIdx.x;
+  if (i >= e.n) return;
+
+  // ---- every column up front: one memory round trip ----------------------
+  StepCtx s;
+  s.i = i;
+  const int act = actions[i];
+  s.B = e.board[i];
+  s.hand = e.hand[i];
+  s.score = e.score[i];
+  s.combo = e.combo[i];
+  s.max_combo = e.max_combo[i];
+  s.moves = e.moves[i];
+  s.lines_tot = e.lines[i];
+  s.blocks = e.blocks[i];
+  s.prev = e.prev[i];
+  s.rng.hi = e.rng_hi[i];
+  s.rng.lo = e.rng_lo[i];
+  s.rng.buf = e.rng_buf[i];
+  s.rng.inc_hi = e.inc_hi[i];
+  s.rng.inc_lo = e.inc_lo[i];
+  s.seed_hi = e.seed_hi[i];
+  s.seed_lo = e.seed_lo[i];
+  s.has_seed = e.has_seed[i] != 0;
+  s.rng.has = hand_has32(s.hand);
+  s.drew = false;
+  s.nblk = 0;
+  s.lines = 0;
+  s.cm = 1;
+  s.gained = 0;
+
+  // ---- validity: block_blast_env.py:237-245 -> engine.py:326-346 ----------
+  const int p = act >> 6;     // a // 64 for a >= 0
+  const int cell = act & 63;  // r*8 + c
+  uint32_t used = hand_used(s.hand);
+  bool valid = act >= 0 && act < 192 && !hand_over(s.hand) && !((used >> p) & 1u);
+  PieceRow pr{};
+  if (valid) {
+    pr = t.row[hand_id(s.hand, p)];
+    valid = ((pr.anchors >> cell) & 1ull) && ((pr.shape << cell) & s.B) == 0;
+  }
+  s.valid = valid;
+
+  if (valid) {
+    // ---- make_move: engine.py:406-429 ------------------------------------
+    s.nblk = (int)pr.ncells;
+    used |= 1u << p;
+    s.moves += 1;
+    s.blocks += s.nblk;
+    int rows, cols;
+    s.B = clear_full(s.B | (pr.shape << cell), rows, cols);
+    s.lines = rows + cols;
+    if (s.lines > 0) {
+      s.combo += 1;
+      s.max_combo = s.combo > s.max_combo ? s.combo : s.max_combo;
+      s.lines_tot += s.lines;
+      s.cm = s.lines < 4 ? s.lines : 4;
+      const int streak = s.combo + 1 < 8 ? s.combo + 1 : 8;  // post-increment combo (engine.py:261)
+      s.gained = s.nblk + (int64_t)(s.lines * 8 * 10) * s.cm * streak;  // blocks_in_lines = lines*8 (engine.py:427)
+    } else {
+      s.combo = 0;
+      s.gained = s.nblk;
+    }
+    s.score += s.gained;
+    uint32_t ids = s.hand & 0x3FFFFu;
+    if (used == 7u) {
+      // ---- all three used -> new hand (engine.py:432-437) ---------------
+      used = 0;
+      s.drew = true;
+      int attempt = 0;
+      bool done;
+      if (a.dbg & 1) {  // diagnostics only: first draw, no solvability test (NOT reference semantics)
+        ids = draw_piece(s.rng);
+        ids |= draw_piece(s.rng) << 6;
+        ids |= draw_piece(s.rng) << 12;
+        done = true;
+      } else if (a.lane_budget <= 0) {
+        done = false;  // default: every search runs wave-cooperatively in escalate_kernel
+      } else {
+        const uint64_t c0 = (a.dbg & 2) ? __builtin_amdgcn_s_memtime() : 0;
+        done = gen_hand_lane(s.B, s.rng, ids, attempt, t.row, t.d, a.lane_budget);
+        if (a.dbg & 2) {
+          a.dbg_out[4 * i + 0] = __builtin_amdgcn_s_memtime() - c0;
+          a.dbg_out[4 * i + 1] = (uint64_t)attempt | ((uint64_t)(!done) << 32);
+          a.dbg_out[4 * i + 2] = 0;
+          a.dbg_out[4 * i + 3] = s.B;
+        }
+      }
+      s.hand = ids | ((uint32_t)s.rng.has << 22);
+      if (!done) {
+        // park: post-move state + the unfinished attempt for escalate_kernel
+        e.board[i] = s.B;
+        e.hand[i] = s.hand;
+        e.rng_hi[i] = s.rng.hi;
+        e.rng_lo[i] = s.rng.lo;
+        e.rng_buf[i] = s.rng.buf;
+        e.score[i] = s.score;
+        e.combo[i] = s.combo;
+        e.max_combo[i] = s.max_combo;
+        e.moves[i] = s.moves;
+        e.lines[i] = s.lines_tot;
+        e.blocks[i] = s.blocks;
+        e.pscratch[i] = pack_pending(attempt, s.nblk, s.lines, s.cm, s.gained);
+        e.pend[i] = 1;
+        return;
+      }
+    } else {
+      s.hand = ids | (used << 18) | (s.hand & (1u << 22));
+    }
+  }
+  finalize(t, e, s, a);
+}
+
+// ---------------------------------------------------------------------------
+// escalation: finish parked envs with a whole wave each
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
+                                                             StepArgs a) {
+  __shared__ Tables t;
+  __shared__ SlowLds slow[kEscBlock / 64];
+  stage_tables(t, g_rows, g_d);
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * kEscBlock + threadIdx.x) >> 6;
+  const int base = wave * kEscGroup;
+  const int mine = base + lane;
+  const bool flagged = lane < kEscGroup && mine < e.n && e.pend[mine] != 0;
+  const uint64_t parked = __ballot(flagged);
+  if (!parked) return;
+  // owner lane k holds env base+k: all of its columns in one round trip
+  StepCtx s;
+  uint64_t pr = 0;
+  if (flagged) {
+    s.i = mine;
+    s.valid = true;
+    s.drew = true;
+    s.B = e.board[mine];
+    const uint32_t h = e.hand[mine];
+    s.rng.hi = e.rng_hi[mine];
+    s.rng.lo = e.rng_lo[mine];
+    s.rng.buf = e.rng_buf[mine];
+    s.rng.inc_hi = e.inc_hi[mine];
+    s.rng.inc_lo = e.inc_lo[mine];
+    s.rng.has = hand_has32(h);
+    pr = e.pscratch[mine];
+    s.score = e.score[mine];
+    s.combo = e.combo[mine];
+    s.max_combo = e.max_combo[mine];
+    s.moves = e.moves[mine];
+    s.lines_tot = e.lines[mine];
+    s.blocks = e.blocks[mine];
+    s.prev = e.prev[mine];
+    s.seed_hi = e.seed_hi[mine];
+    s.seed_lo = e.seed_lo[mine];
+    s.has_seed = e.has_seed[mine] != 0;
+    s.nblk = (int)((pr >> 8) & 0xFFu);
+    s.lines = (int)((pr >> 16) & 0xFFu);
+    s.cm = (int)((pr >> 24) & 0xFFu);
+    s.gained = (int64_t)(uint32_t)(pr >> 32);
+  }
+  // one parked env at a time, searched by the whole wave (register broadcast)
+  uint32_t my_ids = 0;
+  uint64_t it = parked;
+  while (it) {
+    const int k = __ffsll((unsigned long long)it) - 1;
+    it &= it - 1;
+    Pcg w;
+    w.hi = __shfl(s.rng.hi, k);
+    w.lo = __shfl(s.rng.lo, k);
+    w.inc_hi = __shfl(s.rng.inc_hi, k);
+    w.inc_lo = __shfl(s.rng.inc_lo, k);
+    w.buf = __shfl(s.rng.buf, k);
+    w.has = __shfl((int)s.rng.has, k) != 0;
+    const uint64_t wB = __shfl(s.B, k);
+    const int watt = __shfl((int)(pr & 0xFFu), k);
+    uint32_t ids = 0;
+    const uint64_t c0 = (a.dbg & 2) ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t st[4] = {0, 0, 0, 0};
+    gen_hand_wave(wB, w, ids, watt, t.row, t.d, lane, &slow[threadIdx.x >> 6], (a.dbg & 2) ? st : nullptr);
+    if ((a.dbg & 2) && lane == 0) {
+      a.dbg_out[4 * (base + k) + 2] = __builtin_amdgcn_s_memtime() - c0;
+      a.dbg_out[4 * (base + k) + 1] = (uint64_t)st[0] | ((uint64_t)st[1] << 16) | ((uint64_t)st[2] << 32) |
+                                      ((uint64_t)st[3] << 48);
+      a.dbg_out[4 * (base + k) + 3] = wB;
+    }
+    if (lane == k) {
+      s.rng = w;
+      my_ids = ids;
+    }
+  }
+  // finalise every parked env in parallel (its owner lane)
+  if (flagged) {
+    s.hand = my_ids | ((uint32_t)s.rng.has << 22);
+    finalize(t, e, s, a);
+    e.pend[mine] = 0;
   }
 }
 
@@ -331,8 +460,8 @@ __device__ __forceinline__ uint64_t plane_of(const PieceRow* rows, uint64_t boar
 
 // x[N][4][64] f32: 64 chunks per env.
 __global__ void expand_x_kernel(const uint64_t* __restrict__ board, const uint32_t* __restrict__ hand,
-                                const int64_t* __restrict__ index, const PieceRow* __restrict__ g_rows,
-                                int n, float4* __restrict__ x) {
+                                const int64_t* __restrict__ index, const PieceRow* __restrict__ g_rows, int n,
+                                float4* __restrict__ x) {
   __shared__ PieceRow rows[kPieces];
   if (threadIdx.x < kPieces) rows[threadIdx.x] = g_rows[threadIdx.x];
   __syncthreads();
@@ -348,8 +477,8 @@ __global__ void expand_x_kernel(const uint64_t* __restrict__ board, const uint32
 }
 
 // mask f32 [N][192]: 48 chunks per env; int8 [N][192]: 12 chunks of 16 B.
-__global__ void expand_mask_kernel(const uint64_t* __restrict__ mbits, const int64_t* __restrict__ index,
-                                   int n, float4* __restrict__ mf, int4* __restrict__ mi) {
+__global__ void expand_mask_kernel(const uint64_t* __restrict__ mbits, const int64_t* __restrict__ index, int n,
+                                   float4* __restrict__ mf, int4* __restrict__ mi) {
   const int64_t totf = mf ? (int64_t)n * 48 : 0;
   const int64_t toti = mi ? (int64_t)n * 12 : 0;
   for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < totf + toti;
@@ -412,13 +541,20 @@ static inline int grid_for(int64_t units, int block) {
 
 hipError_t launch_reset(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const uint8_t* sel,
                         hipStream_t s) {
-  hipLaunchKernelGGL(reset_kernel, dim3((e.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, e, rows, d, sel);
+  hipLaunchKernelGGL(reset_kernel, dim3((e.n + kStepBlock - 1) / kStepBlock), dim3(kStepBlock), 0, s, e, rows, d,
+                     sel);
   return hipGetLastError();
 }
 
 hipError_t launch_step(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const int32_t* actions,
                        const StepArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(step_kernel, dim3((e.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, e, rows, d, actions, a);
+  hipLaunchKernelGGL(step_kernel, dim3((e.n + kStepBlock - 1) / kStepBlock), dim3(kStepBlock), 0, s, e, rows, d,
+                     actions, a);
+  hipError_t st = hipGetLastError();
+  if (st != hipSuccess) return st;
+  const int envs_per_block = kEscBlock / 64 * kEscGroup;
+  hipLaunchKernelGGL(escalate_kernel, dim3((e.n + envs_per_block - 1) / envs_per_block), dim3(kEscBlock), 0, s, e,
+                     rows, d, a);
   return hipGetLastError();
 }
 

@@ -32,12 +32,18 @@ struct EnvDev {
   uint64_t* seed_hi;    // state right after default_rng(seed_value)
   uint64_t* seed_lo;
   uint8_t* has_seed;    // seed_value is not None -> re-seed on reset
+  uint8_t* pend;        // parked by step_kernel, finished by escalate_kernel
+  uint64_t* pscratch;   // parked env's unfinished attempt + move summary
 };
 
 struct StepArgs {
   bb_reward_cfg cfg;
   double center_tenth;  // reward_config['center_bonus'] * 0.1 (block_blast_env.py:190)
   int autoreset;
+  int lane_budget;      // per-lane solver budget before wave escalation
+  int dbg;              // diagnostics only (BB_DEBUG_MODE): bit0 = skip solvability test,
+                        // bit1 = write per-env solver counters to dbg_out
+  uint64_t* dbg_out;    // [n][4]: lane cycles, attempts | escalated << 32, wave cycles, board
   float* reward;
   uint8_t* terminated;
   double* reward_f64;

@@ -36,6 +36,14 @@ void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces])
       for (int c = 0; c <= 8 - w; ++c) anchors |= 1ull << (r * 8 + c);
     uint64_t packed = 0;
     for (int j = 0; j < 9; ++j) packed |= (uint64_t)offs[p][j < k ? j : 0] << (6 * j);
+    uint64_t ylo = 0, yhi = 0;
+    for (int j = 0; j < k; ++j) {
+      const int bit = 64 - offs[p][j];
+      if (bit >= 64) yhi |= 1ull << (bit - 64);
+      else ylo |= 1ull << bit;
+    }
+    rows[p].ym_lo = ylo;
+    rows[p].ym_hi = yhi;
     rows[p].shape = s;
     rows[p].anchors = anchors;
     rows[p].offs = packed;

@@ -174,6 +174,12 @@ int bb_snapshot(bb_env* env, uint64_t* d_board, uint32_t* d_hand, uint64_t* d_ma
 int bb_get_state(bb_env* env, const bb_state_view* h_view);
 int bb_set_state(bb_env* env, const bb_state_view* h_view);
 
+/* Diagnostics: per-env hand-search counters of the last bb_step, [N][4] =
+ * {in-lane cycles, attempts | escalated << 32, wave cycles, board}.  Only
+ * available when the env was created with BB_DEBUG_MODE having bit 1 set;
+ * reading clears them. */
+int bb_debug_counters(bb_env* env, uint64_t* h_out);
+
 /* Synthetic random policy on its own (see bb_step_out.next_action). */
 int bb_random_actions(const uint64_t* d_mask_bits, int32_t n, uint64_t seed,
                       uint64_t step, uint64_t env_offset, int32_t* d_actions,

@@ -81,6 +81,17 @@ def test_vec_env_bit_exact_custom_rewards(cuda):
     _run_parity(n=64, steps=120, seed=7, p_invalid=0.05, reward_config=rc, act_seed=3)
 
 
+@pytest.mark.parametrize("budget", ["0", "1", "64", "1000000000"])
+def test_vec_env_solver_paths(cuda, monkeypatch, budget):
+    """Budget 0 (default) sends every hand search to the wave-cooperative
+    escalation kernel, 1 / 64 escalate after a partial in-lane search, a huge
+    budget keeps every search inside its lane.  All must reproduce the oracle
+    bit for bit."""
+    monkeypatch.setenv("BB_LANE_BUDGET", budget)
+    terms = _run_parity(n=64, steps=120, seed=4242, p_invalid=0.05, act_seed=9)
+    assert terms > 20
+
+
 def test_vec_env_all_invalid_and_edge_actions(cuda):
     _run_parity(n=16, steps=20, seed=123, p_invalid=1.0, act_seed=5)
 

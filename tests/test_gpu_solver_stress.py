@@ -1,0 +1,99 @@
+"""GPU parity of the hand generator on crowded boards.
+
+Random 45-80 % filled boards where the last unused slot holds SINGLE: placing
+it triggers _generate_new_pieces (engine.py:155-172) on a crowded board, where
+many 3-draw attempts fail (and some envs exhaust all 100 attempts and keep the
+last hand).  The device result (hand, pcg state, score, reward, game over)
+must equal the oracle's reference DFS exactly; this drives both the per-lane
+solver and the wave-cooperative escalation kernel.
+"""
+import numpy as np
+import pytest
+
+from oracle import bb_game as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(rng, fill):
+    if fill < 0:
+        # two isolated holes per row/column: almost no hand fits -> attempts
+        # run to the 100 limit (last hand kept) and most envs end the game
+        while True:
+            grid = np.ones((8, 8), dtype=np.int8)
+            p1, p2 = rng.permutation(8), rng.permutation(8)
+            if np.any(p1 == p2):
+                continue
+            grid[np.arange(8), p1] = 0
+            grid[np.arange(8), p2] = 0
+            if (grid.sum(axis=0) == 6).all():
+                break
+        empties = np.argwhere(grid == 0)
+        r, c = empties[rng.integers(len(empties))]
+        return grid, int(r), int(c)
+    grid = (rng.random((8, 8)) < fill).astype(np.int8)
+    # no full line on the start board (the reference never holds one)
+    for r in range(8):
+        if grid[r].all():
+            grid[r, rng.integers(8)] = 0
+    for c in range(8):
+        if grid[:, c].all():
+            grid[rng.integers(8), c] = 0
+    empties = np.argwhere(grid == 0)
+    r, c = empties[rng.integers(len(empties))]
+    return grid, int(r), int(c)
+
+
+@pytest.mark.parametrize("fill", [0.45, 0.6, 0.7, 0.8, 0.9, 0.95, -1.0])
+def test_crowded_board_hand_generation(cuda, fill):
+    from runtime.device_env import DeviceEnvBatch
+
+    n = 512
+    rng = np.random.default_rng(int(fill * 100) + 1000)
+    dev = DeviceEnvBatch(n, seeds=[5000 + i for i in range(n)], device=cuda)
+    boards = np.zeros(n, np.uint64)
+    hands = np.zeros(n, np.uint32)
+    acts = np.zeros(n, np.int32)
+    refs = []
+    for i in range(n):
+        grid, r, c = _case(rng, fill)
+        a, b = (int(x) for x in rng.integers(0, 37, 2))
+        boards[i] = O.grid_to_u64(grid.tolist())
+        hands[i] = a | (b << 6) | (0 << 12) | (0b011 << 18)
+        acts[i] = 128 + r * 8 + c
+        env = O.Env(seed=5000 + i)
+        env.engine.grid = grid.tolist()
+        env.engine.hand = [a, b, 0]
+        env.engine.used = [True, True, False]
+        env.engine.rng = np.random.default_rng(5000 + i)
+        refs.append(env)
+    dev.set_state(board=boards, hand=hands, prev_holes=np.zeros(n), prev_center=np.zeros(n))
+    import torch
+
+    act_t = torch.from_numpy(acts).to(cuda)
+    dev.step(act_t, want_f64=True, want_info=True)
+    st = dev.state()
+    rew = dev.reward_f64.cpu().numpy()
+    term = dev.terminated.cpu().numpy()
+    info = dev.info_host()
+    attempts = []
+    for i, env in enumerate(refs):
+        _, r_ref, t_ref, _, inf = env.step(int(acts[i]))
+        attempts.append(env.engine.attempts_last)
+        assert rew[i] == r_ref, i
+        assert bool(term[i]) == t_ref, i
+        assert info[i]["score"] == inf["score"]
+        if not t_ref:
+            h = int(st["hand"][i])
+            assert [(h >> (6 * s)) & 63 for s in range(3)] == env.engine.hand, i
+            s = env.engine.rng.bit_generator.state
+            assert (int(st["rng"][i, 0]) << 64 | int(st["rng"][i, 1])) == s["state"]["state"], i
+            assert bool((h >> 22) & 1) == bool(s["has_uint32"]), i
+            if s["has_uint32"]:
+                assert int(st["rng"][i, 2]) == s["uinteger"], i
+        else:  # terminated -> auto-reset happened; the terminal hand is in info
+            h = int(info[i]["term_hand"])
+            assert [(h >> (6 * s)) & 63 for s in range(3)] == env.engine.hand, i
+    attempts = np.array(attempts)
+    assert attempts.max() > 1  # the crowded boards really exercised rejection sampling
+    dev.close()
