@@ -24,6 +24,7 @@ struct bb_env {
   EnvDev d{};
   PieceRow* d_rows = nullptr;
   uint8_t* d_dtab = nullptr;
+  JumpRow* d_jump = nullptr;
   void* slab = nullptr;
   int lane_budget = 0;  // 0: every hand search runs wave-cooperatively (escalate_kernel)
   int dbg = 0;
@@ -86,6 +87,7 @@ size_t slab_bytes(int n) {
   add(n, 8);      // pscratch
   add(kPieces, sizeof(PieceRow));
   add(kPieces * kPieces, 1);
+  add(kJumpMax + 1, sizeof(JumpRow));
   return b;
 }
 
@@ -157,11 +159,15 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   carve(cur, d.pscratch, n);
   carve(cur, e->d_rows, kPieces);
   carve(cur, e->d_dtab, kPieces * kPieces);
+  carve(cur, e->d_jump, kJumpMax + 1);
   PieceRow rows[kPieces];
   uint8_t dtab[kPieces * kPieces];
+  JumpRow jump[kJumpMax + 1];
   build_piece_tables(rows, dtab);
+  build_jump_table(jump);
   st = hipMemcpy(e->d_rows, rows, sizeof(rows), hipMemcpyHostToDevice);
   if (st == hipSuccess) st = hipMemcpy(e->d_dtab, dtab, sizeof(dtab), hipMemcpyHostToDevice);
+  if (st == hipSuccess) st = hipMemcpy(e->d_jump, jump, sizeof(jump), hipMemcpyHostToDevice);
   if (st != hipSuccess) {
     std::string m = std::string("bb_create: table upload: ") + hipGetErrorString(st);
     (void)hipFree(e->slab);
@@ -243,6 +249,7 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.center_tenth = env->cfg.center_bonus * 0.1;
   a.autoreset = env->autoreset;
   a.lane_budget = env->lane_budget;
+  a.jump = env->d_jump;
   a.dbg = env->dbg;
   a.dbg_out = env->dbg_out;
   a.reward = out->reward;

@@ -36,6 +36,13 @@ struct PieceRow {
   uint32_t pad;
 };
 
+// PCG64 jump-ahead table row c: A^c and S_c = sum_{i<c} A^i (mod 2^128), so
+// the state after c steps is A^c * s + inc * S_c (built on the host).
+constexpr int kJumpMax = 64;
+struct JumpRow {
+  uint64_t a_lo, a_hi, s_lo, s_hi;
+};
+
 // Packed hand word (also the host-visible layout, see bbvec.h bb_state_view).
 __host__ __device__ inline uint32_t hand_id(uint32_t h, int slot) { return (h >> (6 * slot)) & 63u; }
 __host__ __device__ inline uint32_t hand_used(uint32_t h) { return (h >> 18) & 7u; }

@@ -34,7 +34,7 @@ namespace bb {
 constexpr int kStepBlock = 64;
 constexpr int kEscBlock = 256;
 #ifndef BB_ESC_GROUP
-#define BB_ESC_GROUP 16
+#define BB_ESC_GROUP 8
 #endif
 constexpr int kEscGroup = BB_ESC_GROUP;  // envs owned by one escalation wave
 
@@ -365,7 +365,6 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
 __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a) {
   __shared__ Tables t;
-  __shared__ SlowLds slow[kEscBlock / 64];
   stage_tables(t, g_rows, g_d);
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * kEscBlock + threadIdx.x) >> 6;
@@ -423,7 +422,7 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
     uint32_t ids = 0;
     const uint64_t c0 = (a.dbg & 2) ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t st[4] = {0, 0, 0, 0};
-    gen_hand_wave(wB, w, ids, watt, t.row, t.d, lane, &slow[threadIdx.x >> 6], (a.dbg & 2) ? st : nullptr);
+    gen_hand_wave(wB, w, ids, watt, t.row, t.d, a.jump, lane, (a.dbg & 2) ? st : nullptr);
     if ((a.dbg & 2) && lane == 0) {
       a.dbg_out[4 * (base + k) + 2] = __builtin_amdgcn_s_memtime() - c0;
       a.dbg_out[4 * (base + k) + 1] = (uint64_t)st[0] | ((uint64_t)st[1] << 16) | ((uint64_t)st[2] << 32) |

@@ -41,6 +41,7 @@ struct StepArgs {
   double center_tenth;  // reward_config['center_bonus'] * 0.1 (block_blast_env.py:190)
   int autoreset;
   int lane_budget;      // per-lane solver budget before wave escalation
+  const JumpRow* jump;  // PCG64 jump-ahead table [kJumpMax + 1]
   int dbg;              // diagnostics only (BB_DEBUG_MODE): bit0 = skip solvability test,
                         // bit1 = write per-env solver counters to dbg_out
   uint64_t* dbg_out;    // [n][4]: lane cycles, attempts | escalated << 32, wave cycles, board
@@ -72,6 +73,7 @@ hipError_t launch_gae(const float* r, const float* v, const float* d, const floa
 
 // Host helpers (bb_tables.cpp).
 void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces]);
+void build_jump_table(JumpRow rows[kJumpMax + 1]);
 void pcg64_seed_numpy(uint64_t seed, uint64_t out[4]);
 
 }  // namespace bb

@@ -19,9 +19,9 @@
 //       succeed if y at q completes a line (the clear may free room for z):
 //       those few q are checked explicitly.  Same for order z then y.
 //   level 3 is the anchors_of() != 0 test.
-// The per-lane search runs under a work budget; a board that exceeds it is
-// finished by a whole wave (solve_wave: lane l takes level-1 anchor l) in the
-// escalation kernel, so one hard board never serialises a wave of easy ones.
+// gen_hand_wave (bottom) runs the search with a whole wave per env; the
+// per-lane gen_hand_lane (budgeted) is kept for the optional in-lane mode
+// (BB_LANE_BUDGET > 0) and the parity tests that exercise it.
 #pragma once
 #include "bb_device.h"
 
@@ -139,31 +139,6 @@ __device__ __forceinline__ int solve_lane(uint64_t B, const PieceRow* tbl, const
   return 0;
 }
 
-// Whole-wave test of one board (all 64 lanes call it with identical
-// arguments).  Lane l owns level-1 anchor l.
-__device__ __forceinline__ bool solve_wave(uint64_t B, const PieceRow* tbl, const uint8_t* dtab, uint32_t i0,
-                                           uint32_t i1, uint32_t i2, int lane) {
-  const uint32_t ids[3] = {i0, i1, i2};
-#pragma unroll 1
-  for (int f = 0; f < 3; ++f) {
-    const uint32_t fi = ids[f];
-    const uint32_t bi = ids[f == 0 ? 1 : 0];
-    const uint32_t ci = ids[f == 2 ? 1 : 2];
-    const PieceRow pf = tbl[fi];
-    const uint64_t A1 = anchors_of(pf, B);
-    bool ok = false;
-    if ((A1 >> lane) & 1ull) {
-      const PieceRow pb = tbl[bi];
-      const PieceRow pc = tbl[ci];
-      int budget = kUnlimited;
-      const uint64_t B1 = clear_full(B | (pf.shape << lane));
-      ok = solve_pair(B1, pb, pc, dtab[bi * kPieces + ci], budget) == 1;
-    }
-    if (__ballot(ok)) return true;
-  }
-  return false;
-}
-
 // _generate_new_pieces (engine.py:155-172) for one lane, under a budget.
 // attempt: attempts already used (in/out).  Returns true when the hand is
 // final (solvable, or 100 attempts exhausted -> last draw kept).  Returns false
@@ -188,25 +163,6 @@ __device__ __forceinline__ bool gen_hand_lane(uint64_t B, Pcg& rng, uint32_t& id
   return true;
 }
 
-// Wave-cooperative continuation of gen_hand_lane for one env (all 64 lanes
-// call it with identical arguments; on return ids/rng are the final hand and
-// stream state, identical in every lane).
-//
-// Level-1 tasks of an attempt are its (f, p) pairs, f in {0,1,2}, p in
-// anchors(f, B), laid out f-major.  Consecutive attempts are drawn ahead
-// (the PCG stream does not depend on the verdicts) and packed while their
-// tasks fit one wave: a crowded board that fails attempt after attempt has
-// few anchors, so up to kPack attempts are tested in one pass.  Slots are in
-// attempt order, hence the lowest successful lane names the first attempt
-// that the reference's sequential loop would have accepted.  An attempt
-// with more than 64 tasks is processed alone in passes of 64 slots.
-// The batch starts at one attempt and doubles after every fully failed
-// batch, so the common case (attempt accepted at once) never draws ahead.
-// Each pass first runs only the O(1) quick test of every slot; the slot's
-// exact level-2 search (one_order loops) runs only when no quick accept
-// decides the pass, so lanes stuck in long loops never hold up an easy win.
-constexpr int kPack = 8;
-
 // Quick part of solve_pair: 1 accept, 0 reject, 2 undecided (A2/A3 returned).
 __device__ __forceinline__ int pair_quick(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint32_t dbc,
                                           uint64_t& A2, uint64_t& A3) {
@@ -227,188 +183,200 @@ __device__ __forceinline__ int pair_quick(uint64_t B1, const PieceRow& pb, const
   return 2;
 }
 
+// Exact level-2 search of one slot (both orders), written for ILP: the two
+// orders' G accumulations run side by side and every anchor mask is consumed
+// from both ends (lowest and highest set bit) per iteration, so four
+// independent dependency chains share each loop trip.  Same verdict as
+// one_order(y,z) || one_order(z,y).
+__device__ __forceinline__ uint64_t pop_low(uint64_t& x) {
+  const uint64_t b = x & (~x + 1ull);
+  x ^= b;
+  return b;
+}
+__device__ __forceinline__ uint64_t pop_high(uint64_t& x) {
+  if (!x) return 0ull;
+  const uint64_t b = 1ull << (63 - __clzll((long long)x));
+  x ^= b;
+  return b;
+}
+__device__ __forceinline__ uint64_t and_shifted(uint64_t G, uint64_t bit, uint64_t mlo, uint64_t mhi) {
+  return bit ? G & hi_shl(mlo, mhi, __ffsll((unsigned long long)bit) - 1) : G;
+}
+__device__ __forceinline__ bool line_then_fits(uint64_t B1, const PieceRow& first, const PieceRow& second,
+                                               uint64_t bit) {
+  if (!bit) return false;
+  const uint64_t B2 = B1 | (first.shape << (__ffsll((unsigned long long)bit) - 1));
+  return has_full_line(B2) && anchors_of(second, clear_full(B2)) != 0ull;
+}
+
 __device__ __forceinline__ bool pair_slow(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint64_t A2,
                                           uint64_t A3) {
-  int budget = kUnlimited;
-  if (A2 && one_order(B1, pb, pc, A2, A3, budget) == 1) return true;
-  if (A3 && one_order(B1, pc, pb, A3, A2, budget) == 1) return true;
+  // G2: b-anchors at which every c-anchor collides (order b then c); G3 mirror
+  uint64_t m2lo, m2hi, m3lo, m3hi;
+  pair_conflict_mask(pb, pc, m2lo, m2hi);
+  pair_conflict_mask(pc, pb, m3lo, m3hi);
+  uint64_t G2 = ~0ull, G3 = ~0ull;
+  uint64_t it3 = A3, it2 = A2;  // G2 runs over c-anchors, G3 over b-anchors
+  while (it3 | it2) {
+    const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
+    const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
+    G2 = and_shifted(and_shifted(G2, r0, m2lo, m2hi), r1, m2lo, m2hi);
+    G3 = and_shifted(and_shifted(G3, q0, m3lo, m3hi), q1, m3lo, m3hi);
+    if ((A2 & ~G2) | (A3 & ~G3)) return true;
+  }
+  if ((A2 & ~G2) | (A3 & ~G3)) return true;
+  // every first placement blocks every second one: only a line clear helps
+  it2 = A2;
+  it3 = A3;
+  while (it2 | it3) {
+    const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
+    const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
+    if (line_then_fits(B1, pb, pc, q0) | line_then_fits(B1, pb, pc, q1) | line_then_fits(B1, pc, pb, r0) |
+        line_then_fits(B1, pc, pb, r1))
+      return true;
+  }
   return false;
 }
 
-// ---------------------------------------------------------------------------
-// Load-balanced exact level-2 search for every undecided slot of a pass.
-// The per-slot loops of one_order (G = AND over z-anchors, then the line-
-// completing y-anchors) become flat task lists -- (slot, z-anchor) and
-// (slot, y-anchor) -- dealt round-robin to the 64 lanes; per-slot results
-// are combined with LDS atomics.  Cost ~ total tasks / 64 instead of the
-// longest slot's loop.
-// ---------------------------------------------------------------------------
-struct SlowLds {
-  uint64_t B1[64];
-  uint64_t Af[64];   // anchors of the piece placed first in the current order
-  uint64_t As[64];   // anchors of the piece placed second
-  uint64_t G[64];    // AND-accumulator
-  uint64_t Mlo[64], Mhi[64];
-  uint32_t pre[64];  // exclusive prefix of task counts
-  uint32_t ok[64];
-  uint8_t first[64], second[64];
-};
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+// ---------------------------------------------------------------------------
+// Wave-cooperative _generate_new_pieces (engine.py:155-172) for one env: all
+// 64 lanes call it with identical arguments; on return ids/rng are the final
+// hand and stream state, identical in every lane.
+//
+//  * anchors of all 37 pieces on B are computed once, lane x = piece x;
+//  * a batch of attempts is drawn in parallel, lane k = attempt k, by PCG64
+//    jump-ahead (state after c steps = A^c s + inc * S_c, host-built table):
+//    the stream position of every draw is known because each attempt eats
+//    exactly three 32-bit values unless a Lemire rejection occurs (p ~ 5e-9
+//    per draw) -- any rejection in the batch falls back to sequential draws;
+//  * level-1 tasks of an attempt are its (f, p) pairs, f-major; consecutive
+//    attempts are packed while their tasks fit 64 lanes.  Slots are in attempt
+//    order, so the lowest successful lane names the first attempt the
+//    reference's sequential loop would have accepted.  An attempt with more
+//    than 64 tasks is processed alone in passes of 64 slots;
+//  * each pass first runs the O(1) quick test of every slot (quick accept +
+//    the reference DFS's first leaf); the exact level-2 search runs only
+//    for slots of attempts that the quick tests leave undecided;
+//  * the batch starts at one attempt and doubles after each failed batch.
+// ---------------------------------------------------------------------------
+constexpr int kPack = 32;
+static_assert(3 * kPack / 2 + 2 <= kJumpMax, "jump table too short for the batch size");
+
+__device__ __forceinline__ void mul128(uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi, uint64_t& lo,
+                                       uint64_t& hi) {
+  lo = alo * blo;
+  hi = __umul64hi(alo, blo) + alo * bhi + ahi * blo;
 }
 
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t& total) {
-  uint32_t x = v;
+__device__ __forceinline__ uint64_t xsl_rr(uint64_t hi, uint64_t lo) {
+  const uint64_t x = hi ^ lo;
+  const unsigned rot = (unsigned)(hi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+// Draw attempt k of a batch starting at stream state s0 without touching s0.
+// Returns true when a Lemire rejection would have shifted the stream.
+__device__ __forceinline__ bool draw_attempt_jump(const Pcg& s0, const JumpRow* J, int k, uint32_t& ids,
+                                                  Pcg& after) {
+  constexpr uint64_t ML = 0x4385DF649FCCF645ull, MH = 0x2360ED051FC65DA4ull;
+  const int h = s0.has ? 1 : 0;
+  const int v0 = 3 * k;
+  const int cfirst = v0 >= h ? (v0 - h) / 2 + 1 : 1;
+  const JumpRow j = J[cfirst];
+  uint64_t l1, h1, l2, h2;
+  mul128(j.a_lo, j.a_hi, s0.lo, s0.hi, l1, h1);
+  mul128(j.s_lo, j.s_hi, s0.inc_lo, s0.inc_hi, l2, h2);
+  const uint64_t c_lo = l1 + l2;
+  const uint64_t c_hi = h1 + h2 + (c_lo < l1 ? 1ull : 0ull);
+  uint64_t n_lo, n_hi;  // one more LCG step
+  mul128(c_lo, c_hi, ML, MH, n_lo, n_hi);
+  n_lo += s0.inc_lo;
+  n_hi += s0.inc_hi + (n_lo < s0.inc_lo ? 1ull : 0ull);
+  const uint64_t o1 = xsl_rr(c_hi, c_lo);
+  const uint64_t o2 = xsl_rr(n_hi, n_lo);
+  bool rej = false;
+  ids = 0;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_up(x, o);
-    if (lane >= o) x += u;
+  for (int d = 0; d < 3; ++d) {
+    const int v = v0 + d;
+    uint32_t val;
+    if (v < h) {
+      val = s0.buf;
+    } else {
+      const int c = (v - h) / 2 + 1;
+      const uint64_t o = c == cfirst ? o1 : o2;
+      val = ((v - h) & 1) ? (uint32_t)(o >> 32) : (uint32_t)o;
+    }
+    const uint64_t m = (uint64_t)val * 37ull;
+    rej |= (uint32_t)m < 7u;
+    ids |= (uint32_t)(m >> 32) << (6 * d);
   }
-  total = __shfl(x, 63);
-  return x - v;
+  const int used = v0 + 3 - h;           // values taken from LCG outputs
+  const int calls = (used + 1) / 2;      // == cfirst or cfirst + 1
+  after = s0;
+  const bool second = calls != cfirst;
+  after.lo = second ? n_lo : c_lo;
+  after.hi = second ? n_hi : c_hi;
+  after.has = (used & 1) != 0;
+  after.buf = after.has ? (uint32_t)((second ? o2 : o1) >> 32) : 0u;
+  return rej;
 }
 
-// last slot s < U with pre[s] <= t
-__device__ __forceinline__ int find_slot(const volatile SlowLds* L, int U, uint32_t t) {
-  int lo = 0, hi = U - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (L->pre[mid] <= t) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-// need: this lane owns an undecided slot.  Returns the slot's verdict.
-__device__ __forceinline__ bool pair_slow_wave(SlowLds* L, const PieceRow* tbl, bool need, uint64_t B1,
-                                               uint32_t bi, uint32_t ci, uint64_t A2, uint64_t A3, int lane) {
-  const uint64_t needs = __ballot(need);
-  const int U = __popcll(needs);
-  const int s = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(needs >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)needs, 0u));
-  volatile SlowLds* V = L;
-  bool ok = false;
-#pragma unroll 1
-  for (int order = 0; order < 2; ++order) {
-    const uint32_t fid = order == 0 ? bi : ci;
-    const uint32_t sid = order == 0 ? ci : bi;
-    const uint64_t Af = order == 0 ? A2 : A3;
-    const uint64_t As = order == 0 ? A3 : A2;
-    const bool active = need && !ok && Af != 0ull;
-    if (!__ballot(active)) continue;
-    // ---- phase G: G[s] = AND_{r in As} (r - D(first, second)) ----------
-    uint32_t cnt = 0;
-    if (active) {
-      uint64_t mlo, mhi;
-      pair_conflict_mask(tbl[fid], tbl[sid], mlo, mhi);
-      V->B1[s] = B1;
-      V->Af[s] = Af;
-      V->As[s] = As;
-      V->G[s] = ~0ull;
-      V->Mlo[s] = mlo;
-      V->Mhi[s] = mhi;
-      V->ok[s] = 0u;
-      V->first[s] = (uint8_t)fid;
-      V->second[s] = (uint8_t)sid;
-      cnt = (uint32_t)__popcll(As);
-    }
-    uint32_t T;
-    const uint32_t pre = wave_excl_scan(cnt, lane, T);
-    // zero-count slots share the next slot's prefix; find_slot takes the last
-    // slot with pre <= t, which is always one that owns task t
-    if (need) V->pre[s] = pre;
-    wave_sync();
-    for (uint32_t t = (uint32_t)lane; t < T; t += 64) {
-      const int k = find_slot(V, U, t);
-      const uint32_t idx = t - V->pre[k];
-      const int r = select_bit(V->As[k], idx);
-      atomicAnd((unsigned long long*)&L->G[k], (unsigned long long)hi_shl(V->Mlo[k], V->Mhi[k], r));
-    }
-    wave_sync();
-    bool undecided = false;
-    if (active) {
-      if (Af & ~V->G[s]) ok = true;
-      else undecided = true;
-    }
-    // ---- phase Q: y-anchors that complete a line (all of Af lies in G) --
-    cnt = undecided ? (uint32_t)__popcll(Af) : 0u;
-    const uint32_t pre2 = wave_excl_scan(cnt, lane, T);
-    if (T == 0) continue;
-    if (need) V->pre[s] = pre2;
-    wave_sync();
-    for (uint32_t t = (uint32_t)lane; t < T; t += 64) {
-      const int k = find_slot(V, U, t);
-      const uint32_t idx = t - V->pre[k];
-      const int q = select_bit(V->Af[k], idx);
-      const uint64_t B2 = V->B1[k] | (tbl[V->first[k]].shape << q);
-      if (has_full_line(B2) && anchors_of(tbl[V->second[k]], clear_full(B2))) V->ok[k] = 1u;
-    }
-    wave_sync();
-    if (undecided && V->ok[s]) ok = true;
-  }
-  return ok;
-}
-
-// stats (diagnostics, may be null): [0] attempts consumed, [1] passes,
-// [2] passes that ran the slow path, [3] max slots of a pass.
 __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& ids, int attempt,
-                                              const PieceRow* tbl, const uint8_t* dtab, int lane,
-                                              SlowLds* slow, uint32_t* stats = nullptr) {
+                                              const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
+                                              int lane, uint32_t* stats = nullptr) {
   const int attempt0 = attempt;
-  // batch entry j lives in lane j's registers
-  uint32_t e_ids = 0;
-  uint64_t e_A0 = 0, e_A1 = 0, e_A2 = 0;
-  int e_off = 0;
-  uint64_t e_hi = 0, e_lo = 0;
-  uint32_t e_buf = 0;
-  int e_has = 0;
+  // anchors of every piece on B: lane x holds piece x
+  const uint64_t acache = lane < kPieces ? anchors_of(tbl[lane], B) : 0ull;
   uint32_t last_ids = ids;
   int pack = 1;
 #pragma unroll 1
   while (attempt < kMaxAttempts) {
-    // ---- build a batch -------------------------------------------------
-    int nb = 0, total = 0;
-#pragma unroll 1
-    while (nb < pack && attempt + nb < kMaxAttempts) {
-      const Pcg before = rng;
-      const uint32_t a = draw_piece(rng);
-      const uint32_t b = draw_piece(rng);
-      const uint32_t c = draw_piece(rng);
-      const uint64_t A0 = anchors_of(tbl[a], B);
-      const uint64_t A1 = anchors_of(tbl[b], B);
-      const uint64_t A2 = anchors_of(tbl[c], B);
-      const int S = __popcll(A0) + __popcll(A1) + __popcll(A2);
-      if (nb > 0 && total + S > 64) {
-        rng = before;  // does not fit: redrawn as the first attempt of the next batch
-        break;
-      }
-      if (lane == nb) {
+    // ---- draw a batch: lane k = attempt k --------------------------------
+    const int kb = pack < kMaxAttempts - attempt ? pack : kMaxAttempts - attempt;
+    uint32_t e_ids = 0;
+    Pcg e_after = rng;
+    bool rej = false;
+    if (lane < kb) rej = draw_attempt_jump(rng, J, lane, e_ids, e_after);
+    int nb_draw = kb;
+    if (__ballot(rej)) {  // rare: redo one attempt with sequential draws
+      Pcg s = rng;
+      const uint32_t a = draw_piece(s), b = draw_piece(s), c = draw_piece(s);
+      if (lane == 0) {
         e_ids = a | (b << 6) | (c << 12);
-        e_A0 = A0;
-        e_A1 = A1;
-        e_A2 = A2;
-        e_off = total;
-        e_hi = rng.hi;
-        e_lo = rng.lo;
-        e_buf = rng.buf;
-        e_has = rng.has;
+        e_after = s;
       }
-      total += S;
-      ++nb;
-      if (total >= 64) break;
+      nb_draw = 1;
     }
-    // ---- test it: passes of 64 slots ------------------------------------
+    const uint64_t eA0 = __shfl(acache, (int)hand_id(e_ids, 0));
+    const uint64_t eA1 = __shfl(acache, (int)hand_id(e_ids, 1));
+    const uint64_t eA2 = __shfl(acache, (int)hand_id(e_ids, 2));
+    const uint32_t S = lane < nb_draw ? (uint32_t)(__popcll(eA0) + __popcll(eA1) + __popcll(eA2)) : 0u;
+    uint32_t incl = S;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
+    }
+    const int e_off = (int)(incl - S);
+    // attempts packed into this pass: the leading ones whose tasks fit 64
+    int nb = __popcll(__ballot(lane < nb_draw && incl <= 64u));
+    if (nb == 0) nb = 1;
+    const int total = (int)__shfl(incl, nb - 1);
+    // ---- test the batch: passes of 64 slots ------------------------------
 #pragma unroll 1
     for (int base = 0; base < total; base += 64) {
       const int slot = base + lane;
-      int j = 0;
-      for (int k = 1; k < nb; ++k)
-        if (__shfl(e_off, k) <= slot) j = k;
-      // cross-lane reads stay outside divergent code: ds_bpermute returns
-      // garbage for source lanes that are inactive
+      int j = 0;  // last packed attempt with e_off <= slot
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1) {
+        const int cand = j + step;
+        const int off = __shfl(e_off, cand < nb ? cand : 0);
+        if (cand < nb && off <= slot) j = cand;
+      }
       const uint32_t jid = __shfl(e_ids, j);
-      const uint64_t jA0 = __shfl(e_A0, j), jA1 = __shfl(e_A1, j), jA2 = __shfl(e_A2, j);
+      const uint64_t jA0 = __shfl(eA0, j), jA1 = __shfl(eA1, j), jA2 = __shfl(eA2, j);
       const int joff = __shfl(e_off, j);
       int q = 0;
       uint64_t B1 = 0, A2 = 0, A3 = 0;
@@ -431,11 +399,9 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
           rem -= c0 + c1;
         }
         const int p = select_bit(Af, (uint32_t)rem);
-        const uint32_t fi = hand_id(jid, f);
         bi = hand_id(jid, f == 0 ? 1 : 0);
         ci = hand_id(jid, f == 2 ? 1 : 2);
-        const PieceRow pf = tbl[fi];
-        B1 = clear_full(B | (pf.shape << p));
+        B1 = clear_full(B | (tbl[hand_id(jid, f)].shape << p));
         q = pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
       }
       // quick accepts decide the pass unless an EARLIER attempt of it is
@@ -451,30 +417,26 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
         const uint32_t sl = (uint32_t)(total - base < 64 ? total - base : 64);
         stats[3] = stats[3] > sl ? stats[3] : sl;
       }
-      if (needs) {
-        const bool r = pair_slow_wave(slow, tbl, need, B1, bi, ci, A2, A3, lane);
-        if (need) ok = r;
-      }
+      if (needs && need) ok = pair_slow(B1, tbl[bi], tbl[ci], A2, A3);
       const uint64_t hit = __ballot(ok);
       if (hit) {
-        const int winner = __ffsll((unsigned long long)hit) - 1;
-        const int jw = __shfl(j, winner);
+        const int jw = __shfl(j, __ffsll((unsigned long long)hit) - 1);
         ids = __shfl(e_ids, jw);
-        rng.hi = __shfl(e_hi, jw);
-        rng.lo = __shfl(e_lo, jw);
-        rng.buf = __shfl(e_buf, jw);
-        rng.has = __shfl(e_has, jw) != 0;
+        rng.hi = __shfl(e_after.hi, jw);
+        rng.lo = __shfl(e_after.lo, jw);
+        rng.buf = __shfl(e_after.buf, jw);
+        rng.has = __shfl((int)e_after.has, jw) != 0;
         if (stats) stats[0] = (uint32_t)(attempt + jw + 1 - attempt0);
         return;
       }
     }
-    // every attempt of the batch failed: continue after its last one
+    // every packed attempt failed: continue after the last one
     const int jl = nb - 1;
     last_ids = __shfl(e_ids, jl);
-    rng.hi = __shfl(e_hi, jl);
-    rng.lo = __shfl(e_lo, jl);
-    rng.buf = __shfl(e_buf, jl);
-    rng.has = __shfl(e_has, jl) != 0;
+    rng.hi = __shfl(e_after.hi, jl);
+    rng.lo = __shfl(e_after.lo, jl);
+    rng.buf = __shfl(e_after.buf, jl);
+    rng.has = __shfl((int)e_after.has, jl) != 0;
     attempt += nb;
     pack = pack * 2 < kPack ? pack * 2 : kPack;
   }

@@ -69,6 +69,20 @@ void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces])
   }
 }
 
+void build_jump_table(JumpRow rows[kJumpMax + 1]) {
+  typedef unsigned __int128 u128;
+  const u128 mult = ((u128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull;
+  u128 a = 1, s = 0;  // A^0, S_0
+  for (int c = 0; c <= kJumpMax; ++c) {
+    rows[c].a_lo = (uint64_t)a;
+    rows[c].a_hi = (uint64_t)(a >> 64);
+    rows[c].s_lo = (uint64_t)s;
+    rows[c].s_hi = (uint64_t)(s >> 64);
+    s += a;
+    a *= mult;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // numpy SeedSequence(seed).generate_state(4, uint64) + PCG64 set_seed:
 // the exact initialisation behind np.random.default_rng(seed)
