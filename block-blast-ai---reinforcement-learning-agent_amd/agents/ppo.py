@@ -1,0 +1,404 @@
+"""Masked PPO on the MI355X: rollout buffers in HBM, fused HIP rollout kernels,
+PyTorch-ROCm CNN update, RCCL gradient all-reduce for data parallelism.
+
+Drop-in for the reference ``src/agents/ppo.py`` (PPOConfig 26-67,
+RolloutBuffer 70-218, PPOAgent 221-449): same class names, constructor
+arguments, method names, return types and checkpoint format.  What changes is
+where the work runs:
+
+* ``RolloutBuffer`` keeps the reference's float32 layout but lives on the
+  device; GAE is the ``bb_gae`` kernel (numpy float32 op order, bit-exact).
+* ``PackedRolloutBuffer`` stores ~60 B per env-step instead of ~1.8 KiB (board
+  bits, hand word, mask bits, ...) and expands minibatches with ``bb_gather_obs``.
+* action sampling / log-prob / masked entropy on the rollout path is the fused
+  ``bb_masked_sample`` kernel (Philox uniforms instead of torch.multinomial).
+* the update is the reference loss (network.py:210-262, ppo.py:362-401); under
+  torch.distributed every optimizer step all-reduces ONE flat gradient buffer
+  (the parameters' .grad are views into it) and advantage moments are global.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Any, Dict, Iterator, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from models.network import BlockBlastNetwork, masked_entropy
+from runtime import kernels as K
+
+from .base import BaseAgent
+
+_EPS32 = float(torch.finfo(torch.float32).eps)  # Categorical clamp_probs
+
+
+@dataclass
+class PPOConfig:
+    """ppo.py:26-67."""
+    learning_rate: float = 3e-4
+    gamma: float = 0.99
+    gae_lambda: float = 0.95
+    clip_epsilon: float = 0.2
+    entropy_coef: float = 0.01
+    value_coef: float = 0.5
+    max_grad_norm: float = 0.5
+    num_epochs: int = 10
+    batch_size: int = 64
+    conv_channels: Tuple[int, ...] = (64, 128, 128)
+    fc_hidden: Tuple[int, ...] = (512, 256)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {
+            "learning_rate": self.learning_rate, "gamma": self.gamma, "gae_lambda": self.gae_lambda,
+            "clip_epsilon": self.clip_epsilon, "entropy_coef": self.entropy_coef, "value_coef": self.value_coef,
+            "max_grad_norm": self.max_grad_norm, "num_epochs": self.num_epochs, "batch_size": self.batch_size,
+            "conv_channels": self.conv_channels, "fc_hidden": self.fc_hidden,
+        }
+
+    @classmethod
+    def from_dict(cls, data: Dict[str, Any]) -> "PPOConfig":
+        return cls(**{k: v for k, v in data.items() if k in cls.__dataclass_fields__})
+
+
+def _world() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def _as_tensor(x, device, dtype) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype, non_blocking=True)
+    return torch.as_tensor(np.asarray(x), dtype=dtype).to(device, non_blocking=True)
+
+
+def _global_moments(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Mean / population std (np.std, ddof 0) over every rank's samples."""
+    if _world() == 1:
+        return x.mean(), x.std(unbiased=False)
+    s = torch.stack([x.double().sum(), (x.double() ** 2).sum(), torch.tensor(float(x.numel()), device=x.device,
+                                                                               dtype=torch.float64)])
+    dist.all_reduce(s)
+    mean = s[0] / s[2]
+    var = (s[1] / s[2] - mean * mean).clamp(min=0.0)
+    return mean.float(), var.sqrt().float()
+
+
+class RolloutBuffer:
+    """ppo.py:70-218 with device storage (float32 layout of the reference)."""
+
+    def __init__(self, buffer_size: int, num_envs: int, board_size: int = 8, num_pieces: int = 3,
+                 action_space_size: int = 192, device: torch.device = torch.device("cpu")):
+        self.buffer_size = buffer_size
+        self.num_envs = num_envs
+        self.device = torch.device(device)
+        d, T, N = self.device, buffer_size, num_envs
+        z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=d)  # noqa: E731
+        self.boards = z(T, N, board_size, board_size)
+        self.pieces = z(T, N, num_pieces, board_size, board_size)
+        self.action_masks = z(T, N, action_space_size)
+        self.actions = z(T, N, dt=torch.int64)
+        self.log_probs = z(T, N)
+        self.rewards = z(T, N)
+        self.dones = z(T, N)
+        self.values = z(T, N)
+        self.advantages = z(T, N)
+        self.returns = z(T, N)
+        self.ptr = 0
+        self.full = False
+
+    def add(self, board, pieces, action_mask, action, log_prob, reward, done, value) -> None:
+        d, t = self.device, self.ptr
+        self.boards[t] = _as_tensor(board, d, torch.float32)
+        self.pieces[t] = _as_tensor(pieces, d, torch.float32)
+        self.action_masks[t] = _as_tensor(action_mask, d, torch.float32)
+        self.actions[t] = _as_tensor(action, d, torch.int64)
+        self.log_probs[t] = _as_tensor(log_prob, d, torch.float32)
+        self.rewards[t] = _as_tensor(reward, d, torch.float32)
+        self.dones[t] = _as_tensor(done, d, torch.float32)
+        self.values[t] = _as_tensor(value, d, torch.float32)
+        self.ptr += 1
+        if self.ptr >= self.buffer_size:
+            self.full = True
+
+    def _gpu(self) -> torch.device:
+        return self.device if self.device.type == "cuda" else torch.device("cuda", 0)
+
+    def compute_returns_and_advantages(self, last_values, gamma: float, gae_lambda: float) -> None:
+        """ppo.py:141-169 as the bb_gae kernel."""
+        g = self._gpu()
+        adv, ret = K.gae(self.rewards.to(g), self.values.to(g), self.dones.to(g),
+                         _as_tensor(last_values, g, torch.float32), gamma, gae_lambda)
+        self.advantages = adv.to(self.device)
+        self.returns = ret.to(self.device)
+
+    def get_samples(self, batch_size: int) -> Iterator[Tuple[torch.Tensor, ...]]:
+        """ppo.py:171-213: flatten, normalise advantages (ppo.py:196), random
+        minibatches from numpy's global permutation (ppo.py:199)."""
+        total = self.buffer_size * self.num_envs
+        boards = self.boards.reshape(total, *self.boards.shape[2:])
+        pieces = self.pieces.reshape(total, *self.pieces.shape[2:])
+        masks = self.action_masks.reshape(total, -1)
+        actions = self.actions.reshape(total)
+        log_probs = self.log_probs.reshape(total)
+        adv = self.advantages.reshape(total)
+        returns = self.returns.reshape(total)
+        mean, std = _global_moments(adv)
+        adv = (adv - mean) / (std + 1e-8)
+        idx = torch.from_numpy(np.random.permutation(total)).to(self.device)
+        for start in range(0, total, batch_size):
+            b = idx[start:start + batch_size]
+            yield (boards[b], pieces[b], masks[b], actions[b], log_probs[b], adv[b], returns[b])
+
+    def reset(self) -> None:
+        self.ptr = 0
+        self.full = False
+
+
+class PackedRolloutBuffer:
+    """Device rollout storage in the env's packed format (~60 B / env-step):
+    board bits, hand word, mask bits, action, log-prob, reward, done, value.
+    Minibatch observations are expanded on the fly by ``bb_gather_obs``."""
+
+    def __init__(self, buffer_size: int, num_envs: int, device: torch.device):
+        self.buffer_size, self.num_envs = buffer_size, num_envs
+        self.device = torch.device(device)
+        T, N, d = buffer_size, num_envs, self.device
+        self.board = torch.zeros((T, N), dtype=torch.int64, device=d)
+        self.hand = torch.zeros((T, N), dtype=torch.int32, device=d)
+        self.mask_bits = torch.zeros((T, N, 3), dtype=torch.int64, device=d)
+        self.actions = torch.zeros((T, N), dtype=torch.int64, device=d)
+        self.log_probs = torch.zeros((T, N), dtype=torch.float32, device=d)
+        self.rewards = torch.zeros((T, N), dtype=torch.float32, device=d)
+        self.dones = torch.zeros((T, N), dtype=torch.float32, device=d)
+        self.values = torch.zeros((T, N), dtype=torch.float32, device=d)
+        self.advantages = torch.zeros((T, N), dtype=torch.float32, device=d)
+        self.returns = torch.zeros((T, N), dtype=torch.float32, device=d)
+        self.ptr = 0
+        self.full = False
+
+    def reset(self) -> None:
+        self.ptr = 0
+        self.full = False
+
+    def advance(self) -> None:
+        self.ptr += 1
+        self.full = self.ptr >= self.buffer_size
+
+    def compute_returns_and_advantages(self, last_values: torch.Tensor, gamma: float, gae_lambda: float) -> None:
+        K.gae(self.rewards, self.values, self.dones, last_values.float(), gamma, gae_lambda,
+              adv=self.advantages, ret=self.returns)
+
+    def get_minibatches(self, batch_size: int, generator: Optional[torch.Generator] = None):
+        """Yields (x (B,4,8,8), mask f32 (B,192), actions, old log-probs,
+        normalised advantages, returns) in a random order."""
+        total = self.buffer_size * self.num_envs
+        adv = self.advantages.reshape(total)
+        mean, std = _global_moments(adv)
+        adv = (adv - mean) / (std + 1e-8)
+        perm = torch.randperm(total, device=self.device, generator=generator)
+        board, hand, mb = self.board.reshape(total), self.hand.reshape(total), self.mask_bits.reshape(total, 3)
+        actions, logp, ret = self.actions.reshape(total), self.log_probs.reshape(total), self.returns.reshape(total)
+        for start in range(0, total, batch_size):
+            b = perm[start:start + batch_size]
+            x, mf = K.gather_obs(board, hand, mb, b)
+            yield x, mf, actions[b], logp[b], adv[b], ret[b]
+
+
+def categorical_log_prob(probs: torch.Tensor, action: torch.Tensor) -> torch.Tensor:
+    """Categorical(probs).log_prob(action) without the validation sync:
+    log(clamp(p / sum p, eps, 1 - eps))[action] (torch clamp_probs)."""
+    p = probs / probs.sum(dim=-1, keepdim=True)
+    return torch.log(p.clamp(min=_EPS32, max=1.0 - _EPS32)).gather(-1, action.unsqueeze(-1)).squeeze(-1)
+
+
+class PPOAgent(BaseAgent):
+    """ppo.py:221-449."""
+
+    def __init__(self, config: Optional[PPOConfig] = None, device: Optional[torch.device] = None,
+                 sample_seed: Optional[int] = None):
+        if device is None:
+            device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        super().__init__(torch.device(device))
+        self.config = config or PPOConfig()
+        self.network = BlockBlastNetwork(conv_channels=self.config.conv_channels,
+                                         fc_hidden=self.config.fc_hidden).to(self.device)
+        self.optimizer = torch.optim.Adam(self.network.parameters(), lr=self.config.learning_rate, eps=1e-5)
+        self.scheduler = None
+        # Philox key for rollout sampling (derived from torch's seeded RNG)
+        self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if sample_seed is None else int(sample_seed)
+        self.sample_step = 0
+        self._flat_grad = None
+        self.autocast_dtype: Optional[torch.dtype] = None  # e.g. torch.bfloat16 for the CNN
+
+    # ------------------------------------------------------------ helpers
+    def _raw(self, x: torch.Tensor):
+        if self.autocast_dtype is not None and x.is_cuda:
+            with torch.autocast("cuda", dtype=self.autocast_dtype):
+                logits, value = self.network.raw(x)
+            return logits.float(), value.float()
+        return self.network.raw(x)
+
+    def _obs_to_device(self, obs: Dict[str, Any]):
+        board = _as_tensor(obs["board"], self.device, torch.float32)
+        pieces = _as_tensor(obs["pieces"], self.device, torch.float32)
+        return BlockBlastNetwork.stack_input(board, pieces)
+
+    def _sample(self, logits: torch.Tensor, mask: torch.Tensor, deterministic: bool, env_offset: int = 0,
+                want_entropy: bool = False):
+        if not logits.is_cuda:
+            raise RuntimeError("PPOAgent rollout sampling runs on the HIP device (no CPU fallback)")
+        mb = K.pack_mask(mask)
+        step = self.sample_step
+        self.sample_step += 1
+        return K.masked_sample(logits, mb, seed=self.sample_seed, step=step, env_offset=env_offset,
+                               deterministic=deterministic, want_entropy=want_entropy)
+
+    # ------------------------------------------------- reference interface
+    def select_action(self, observation: Dict[str, np.ndarray], deterministic: bool = False):
+        """ppo.py:261-289."""
+        with torch.no_grad():
+            x = self._obs_to_device({k: np.asarray(v)[None] for k, v in observation.items()})
+            mask = _as_tensor(np.asarray(observation["action_mask"])[None], self.device, torch.float32)
+            logits, value = self._raw(x)
+            a, lp, ent = self._sample(logits, mask, deterministic, want_entropy=True)
+            return int(a.item()), {"log_prob": float(lp.item()), "entropy": float(ent.item()),
+                                   "value": float(value.item())}
+
+    def select_actions(self, observations: Dict[str, np.ndarray], deterministic: bool = False):
+        """ppo.py:291-319 (numpy in, numpy out)."""
+        with torch.no_grad():
+            x = self._obs_to_device(observations)
+            mask = _as_tensor(observations["action_mask"], self.device, torch.float32)
+            logits, value = self._raw(x)
+            a, lp, _ = self._sample(logits, mask, deterministic)
+            return a.cpu().numpy(), lp.cpu().numpy(), value.cpu().numpy()
+
+    def get_values(self, observations: Dict[str, np.ndarray]) -> np.ndarray:
+        """ppo.py:321-328."""
+        with torch.no_grad():
+            return self._raw(self._obs_to_device(observations))[1].cpu().numpy()
+
+    # ------------------------------------------------------ device fast path
+    def act_device(self, x: torch.Tensor, mask_bits: torch.Tensor, env_offset: int = 0,
+                   deterministic: bool = False):
+        """Rollout step on device tensors: (action int64, log-prob, value)."""
+        with torch.no_grad():
+            logits, value = self._raw(x)
+            step = self.sample_step
+            self.sample_step += 1
+            a, lp, _ = K.masked_sample(logits, mask_bits, seed=self.sample_seed, step=step, env_offset=env_offset,
+                                       deterministic=deterministic, want_entropy=False)
+            return a, lp, value
+
+    def values_device(self, x: torch.Tensor) -> torch.Tensor:
+        with torch.no_grad():
+            return self._raw(x)[1]
+
+    # ------------------------------------------------------------- update
+    def _grad_buffer(self) -> torch.Tensor:
+        """Flat fp32 gradient buffer; every parameter's .grad is a view into it,
+        so one all-reduce covers the whole model (5,290,113 floats)."""
+        if self._flat_grad is None:
+            params = [p for p in self.network.parameters() if p.requires_grad]
+            n = sum(p.numel() for p in params)
+            self._flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
+            off = 0
+            for p in params:
+                p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
+                off += p.numel()
+        return self._flat_grad
+
+    def _minibatch_loss(self, x, masks, actions, old_log_probs, advantages, returns):
+        cfg = self.config
+        logits, values = self._raw(x)
+        masked = logits + torch.where(masks.bool(), torch.zeros_like(logits), torch.full_like(logits, float("-inf")))
+        probs = F.softmax(masked, dim=-1)
+        new_log_probs = categorical_log_prob(probs, actions)
+        entropy = masked_entropy(probs, masks)
+        ratio = torch.exp(new_log_probs - old_log_probs)
+        surr1 = ratio * advantages
+        surr2 = torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon) * advantages
+        policy_loss = -torch.min(surr1, surr2).mean()
+        value_loss = F.mse_loss(values, returns)
+        entropy_loss = -entropy.mean()
+        loss = policy_loss + cfg.value_coef * value_loss + cfg.entropy_coef * entropy_loss
+        with torch.no_grad():
+            approx_kl = ((ratio - 1) - torch.log(ratio)).mean()
+            clip_fraction = ((ratio - 1).abs() > cfg.clip_epsilon).float().mean()
+            stats = torch.stack([policy_loss, value_loss, entropy.mean(), loss, approx_kl, clip_fraction]).detach()
+        return loss, stats
+
+    def _optimizer_step(self, loss: torch.Tensor) -> None:
+        flat = self._grad_buffer()
+        flat.zero_()
+        loss.backward()
+        world = _world()
+        if world > 1:
+            dist.all_reduce(flat)
+            flat.div_(world)
+        nn.utils.clip_grad_norm_(self.network.parameters(), self.config.max_grad_norm)
+        self.optimizer.step()
+
+    def update(self, buffer, last_values, batch_size: Optional[int] = None) -> Dict[str, float]:
+        """ppo.py:330-423.  Metrics are accumulated on the device and read once.
+        ``batch_size`` overrides the per-rank minibatch (data-parallel runs
+        pass config.batch_size // world so the global minibatch is unchanged)."""
+        cfg = self.config
+        bs = int(batch_size or cfg.batch_size)
+        if isinstance(last_values, np.ndarray):
+            last_values = torch.from_numpy(last_values)
+        buffer.compute_returns_and_advantages(last_values, cfg.gamma, cfg.gae_lambda)
+        acc = torch.zeros(6, dtype=torch.float32, device=self.device)
+        n = 0
+        packed = hasattr(buffer, "get_minibatches")
+        for _ in range(cfg.num_epochs):
+            batches = buffer.get_minibatches(bs) if packed else buffer.get_samples(bs)
+            for batch in batches:
+                if packed:
+                    x, masks, actions, old_lp, adv, ret = batch
+                else:
+                    boards, pieces, masks, actions, old_lp, adv, ret = batch
+                    x = BlockBlastNetwork.stack_input(boards.to(self.device), pieces.to(self.device))
+                    masks, actions, old_lp, adv, ret = (t.to(self.device) for t in (masks, actions, old_lp, adv, ret))
+                loss, stats = self._minibatch_loss(x, masks, actions, old_lp, adv, ret)
+                self._optimizer_step(loss)
+                acc += stats
+                n += 1
+        m = (acc / max(n, 1)).tolist()
+        keys = ("policy_loss", "value_loss", "entropy", "total_loss", "approx_kl", "clip_fraction")
+        return dict(zip(keys, m))
+
+    # ----------------------------------------------------------- checkpoint
+    def save(self, path: str) -> None:
+        """ppo.py:425-431 (same dict keys)."""
+        torch.save({"network_state_dict": self.network.state_dict(),
+                    "optimizer_state_dict": self.optimizer.state_dict(),
+                    "config": self.config.to_dict()}, path)
+
+    def load(self, path: str) -> None:
+        """ppo.py:433-439 (safe loader: tensors and plain containers only)."""
+        ckpt = torch.load(path, map_location=self.device, weights_only=True)
+        self.network.load_state_dict(ckpt["network_state_dict"])
+        if "optimizer_state_dict" in ckpt:
+            self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+        if "config" in ckpt:
+            self.config = PPOConfig.from_dict(ckpt["config"])
+        self._flat_grad = None
+
+    def train(self) -> None:
+        super().train()
+        self.network.train()
+
+    def eval(self) -> None:
+        super().eval()
+        self.network.eval()
+
+
+def broadcast_parameters(agent: PPOAgent, src: int = 0) -> None:
+    """Start every data-parallel rank from rank src's weights."""
+    if _world() > 1:
+        for p in agent.network.state_dict().values():
+            dist.broadcast(p, src)

@@ -1,0 +1,150 @@
+"""Policy/value CNN of the Block Blast agent (stays PyTorch-ROCm).
+
+Same architecture, parameter names (``conv_encoder.N.*``, ``fc_encoder.N.*``,
+``policy_head.N.*``, ``value_head.N.*``), initialisation and forward semantics
+as the reference ``src/models/network.py::BlockBlastNetwork`` (network.py:33-271),
+so checkpoints load both ways.  The conv/linear GEMMs run on MFMA through
+PyTorch; the masking / softmax / Categorical / sample / entropy tail of
+``get_action_and_value`` has a fused HIP kernel (``masked_sample`` below,
+csrc/bb_ppo.hip) used on the rollout path.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.distributions import Categorical
+
+N_PARAMS_DEFAULT = 5_290_113  # parameter count of the default net
+
+
+class ResidualBlock(nn.Module):
+    """network.py:14-30: conv-bn-relu-conv-bn + identity, relu."""
+
+    def __init__(self, channels: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
+        self.bn1 = nn.BatchNorm2d(channels)
+        self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
+        self.bn2 = nn.BatchNorm2d(channels)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y = F.relu(self.bn1(self.conv1(x)))
+        y = self.bn2(self.conv2(y))
+        return F.relu(y + x)
+
+
+def _conv_stack(in_ch: int, channels: Sequence[int], batch_norm: bool, residual: bool) -> nn.Sequential:
+    layers = []
+    for i, out_ch in enumerate(channels):
+        layers.append(nn.Conv2d(in_ch, out_ch, kernel_size=3, padding=1))
+        if batch_norm:
+            layers.append(nn.BatchNorm2d(out_ch))
+        layers.append(nn.ReLU())
+        if residual and i > 0:  # network.py:86-87
+            layers.append(ResidualBlock(out_ch))
+        in_ch = out_ch
+    return nn.Sequential(*layers)
+
+
+def _mlp(in_f: int, hidden: Sequence[int]) -> nn.Sequential:
+    layers = []
+    for h in hidden:
+        layers += [nn.Linear(in_f, h), nn.ReLU(), nn.Dropout(0.1)]
+        in_f = h
+    return nn.Sequential(*layers)
+
+
+class BlockBlastNetwork(nn.Module):
+    def __init__(
+        self,
+        board_size: int = 8,
+        num_pieces: int = 3,
+        conv_channels: Tuple[int, ...] = (64, 128, 128),
+        fc_hidden: Tuple[int, ...] = (512, 256),
+        action_space_size: int = 192,
+        use_residual: bool = True,
+        use_batch_norm: bool = True,
+    ):
+        super().__init__()
+        self.board_size = board_size
+        self.num_pieces = num_pieces
+        self.action_space_size = action_space_size
+        self.conv_encoder = _conv_stack(1 + num_pieces, conv_channels, use_batch_norm, use_residual)
+        self.fc_encoder = _mlp(conv_channels[-1] * board_size * board_size, fc_hidden)
+        self.policy_head = nn.Sequential(nn.Linear(fc_hidden[-1], 256), nn.ReLU(), nn.Linear(256, action_space_size))
+        self.value_head = nn.Sequential(nn.Linear(fc_hidden[-1], 128), nn.ReLU(), nn.Linear(128, 1))
+        self.apply(self._init_weights)
+
+    @staticmethod
+    def _init_weights(m: nn.Module) -> None:
+        """network.py:122-133: kaiming-uniform (relu) weights, zero biases."""
+        if isinstance(m, (nn.Linear, nn.Conv2d)):
+            nn.init.kaiming_uniform_(m.weight, nonlinearity="relu")
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+
+    # ------------------------------------------------------------------ core
+    def trunk(self, x: torch.Tensor) -> torch.Tensor:
+        """x: (B, 4, 8, 8) -> fc features (B, fc_hidden[-1])."""
+        h = self.conv_encoder(x)
+        return self.fc_encoder(h.reshape(h.shape[0], -1))
+
+    def raw(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Unmasked logits (B, 192) and value (B,) from the stacked input."""
+        h = self.trunk(x)
+        return self.policy_head(h), self.value_head(h).squeeze(-1)
+
+    @staticmethod
+    def stack_input(board: torch.Tensor, pieces: torch.Tensor) -> torch.Tensor:
+        if board.dim() == 3:
+            board = board.unsqueeze(1)
+        return torch.cat([board, pieces], dim=1)
+
+    # ------------------------------------------------- reference interface
+    def forward(self, board: torch.Tensor, pieces: torch.Tensor,
+                action_mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """network.py:135-182: masked logits (invalid -> -inf) and value."""
+        logits, value = self.raw(self.stack_input(board, pieces))
+        if action_mask is not None:
+            logits = logits + torch.where(action_mask.bool(), torch.zeros_like(logits),
+                                          torch.full_like(logits, float("-inf")))
+        return logits, value
+
+    def get_action_and_value(self, board, pieces, action_mask, action=None, deterministic: bool = False):
+        """network.py:184-230 (torch path; differentiable, used by the update)."""
+        logits, value = self.forward(board, pieces, action_mask)
+        action, log_prob, entropy = categorical_tail(logits, action_mask, action, deterministic)
+        return action, log_prob, entropy, value
+
+    def _masked_entropy(self, probs: torch.Tensor, action_mask: torch.Tensor) -> torch.Tensor:
+        return masked_entropy(probs, action_mask)
+
+    def get_value(self, board: torch.Tensor, pieces: torch.Tensor) -> torch.Tensor:
+        """network.py:264-271."""
+        return self.forward(board, pieces)[1]
+
+
+def masked_entropy(probs: torch.Tensor, action_mask: torch.Tensor) -> torch.Tensor:
+    """network.py:232-262: entropy of the mask-renormalised distribution."""
+    mask = action_mask.bool().float()
+    masked = probs * mask
+    norm = masked / masked.sum(dim=-1, keepdim=True).clamp(min=1e-10)
+    return -(norm * torch.log(norm.clamp(min=1e-10)) * mask).sum(dim=-1)
+
+
+def categorical_tail(masked_logits: torch.Tensor, action_mask: torch.Tensor, action=None,
+                     deterministic: bool = False):
+    """softmax -> Categorical(probs) -> sample/argmax -> log_prob, masked entropy
+    (network.py:210-230), differentiable torch ops."""
+    probs = F.softmax(masked_logits, dim=-1)
+    dist = Categorical(probs=probs)
+    if action is None:
+        action = torch.argmax(probs, dim=-1) if deterministic else dist.sample()
+    return action, dist.log_prob(action), masked_entropy(probs, action_mask)
+
+
+def count_params(net: nn.Module) -> int:
+    return sum(p.numel() for p in net.parameters())

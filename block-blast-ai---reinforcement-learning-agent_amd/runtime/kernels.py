@@ -1,0 +1,107 @@
+"""torch-facing wrappers of the rollout-side HIP kernels (csrc/bb_ppo.hip,
+csrc/bb_env.hip expand).  Inputs/outputs are device tensors; launches go on
+torch's current stream; nothing here falls back to CPU."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import torch
+
+from . import lib as L
+
+_BIT = None
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _s(dev: torch.device):
+    return C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise L.BBNativeError("HIP kernel inputs must be device tensors (no CPU fallback)")
+
+
+def pack_mask(mask: torch.Tensor) -> torch.Tensor:
+    """(N, 192) bool/int/float mask -> (N, 3) int64 bit words (bbvec.h layout)."""
+    global _BIT
+    _need_cuda(mask)
+    if _BIT is None or _BIT.device != mask.device:
+        _BIT = (torch.ones(64, dtype=torch.int64, device=mask.device) << torch.arange(64, device=mask.device))
+    m = (mask.reshape(mask.shape[0], 3, 64) != 0).to(torch.int64)
+    return (m * _BIT).sum(dim=-1)
+
+
+def masked_sample(
+    logits: torch.Tensor,
+    mask_bits: torch.Tensor,
+    uniform: Optional[torch.Tensor] = None,
+    seed: int = 0,
+    step: int = 0,
+    env_offset: int = 0,
+    deterministic: bool = False,
+    action_in: Optional[torch.Tensor] = None,
+    want_entropy: bool = True,
+) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+    """Fused masked softmax / Categorical / sample / log-prob / masked entropy
+    (network.py:173-180, 210-262).  logits f32 (N,192) unmasked; mask_bits
+    int64 (N,3).  Returns (action int64, log_prob f32, entropy f32)."""
+    _need_cuda(logits, mask_bits, uniform, action_in)
+    logits = logits.contiguous().float()
+    n = logits.shape[0]
+    dev = logits.device
+    act = torch.empty(n, dtype=torch.int64, device=dev)
+    logp = torch.empty(n, dtype=torch.float32, device=dev)
+    ent = torch.empty(n, dtype=torch.float32, device=dev) if want_entropy else None
+    if uniform is not None:
+        uniform = uniform.contiguous().float()
+    if action_in is not None:
+        action_in = action_in.contiguous().long()
+    L.check(
+        L.load().bb_masked_sample(_p(logits), _p(mask_bits.contiguous()), n, _p(uniform), seed, step, env_offset,
+                                  int(bool(deterministic)), _p(action_in), _p(act), _p(logp), _p(ent), _s(dev)),
+        "bb_masked_sample",
+    )
+    return (action_in if action_in is not None else act), logp, ent
+
+
+def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, last_values: torch.Tensor,
+        gamma: float, gae_lambda: float, adv: Optional[torch.Tensor] = None,
+        ret: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """RolloutBuffer.compute_returns_and_advantages (ppo.py:141-169) on [T, N]
+    f32 device tensors, numpy-2 float32 op order (gamma*lambda multiplied in
+    double first, as Python does, then rounded to f32)."""
+    _need_cuda(rewards, values, dones, last_values)
+    T, N = rewards.shape
+    adv = torch.empty_like(rewards) if adv is None else adv
+    ret = torch.empty_like(rewards) if ret is None else ret
+    g32 = float(torch.tensor(gamma, dtype=torch.float32))
+    gl32 = float(torch.tensor(gamma * gae_lambda, dtype=torch.float32))
+    L.check(
+        L.load().bb_gae(_p(rewards.contiguous()), _p(values.contiguous()), _p(dones.contiguous()),
+                        _p(last_values.contiguous()), T, N, g32, gl32, _p(adv), _p(ret), _s(rewards.device)),
+        "bb_gae",
+    )
+    return adv, ret
+
+
+def gather_obs(board: torch.Tensor, hand: torch.Tensor, mask_bits: torch.Tensor, index: torch.Tensor,
+               want_x: bool = True, want_mask: bool = True):
+    """Packed rollout records -> network input x (n,4,8,8) f32 and f32 mask
+    (n,192) for the rows in `index` (RolloutBuffer.get_samples, ppo.py:171-213)."""
+    _need_cuda(board, hand, mask_bits, index)
+    n = index.numel()
+    dev = board.device
+    x = torch.empty((n, 4, 8, 8), dtype=torch.float32, device=dev) if want_x else None
+    mf = torch.empty((n, 192), dtype=torch.float32, device=dev) if want_mask else None
+    L.check(
+        L.load().bb_gather_obs(_p(board), _p(hand), _p(mask_bits), _p(index.contiguous().long()), n, _p(x), _p(mf),
+                               _s(dev)),
+        "bb_gather_obs",
+    )
+    return x, mf
