@@ -12,7 +12,9 @@ step kernel).  One "step" = one bb_step launch over the whole batch.
 
 Prints ONE JSON line on rank 0.  `roofline` prices the step kernel against
 HBM with the algorithmic bytes of SURVEY.md 8(d) (194 B per env-step) over its
-average launch duration measured here with HIP events on the launch stream;
+average launch duration measured here with HIP events on the launch stream
+(one bb_step = bb::step_kernel + bb::escalate_kernel, back to back on that
+stream; the rocprofv3 kernel-trace sum of the two agrees, profiles/);
 `cpu_baseline` times the CPU port of the reference's 64-env vectorised path
 (oracle/bb_game.py, one core) on a bounded sample.
 """
@@ -69,7 +71,8 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
 
 def load_traffic(n_envs: int):
     """HBM bytes per step-kernel launch from a committed rocprofv3 PMC run
-    (profiles/pmc_step_kernel.json, written by tools/pmc_traffic.py), or None."""
+    (profiles/pmc_step_kernel.json, written by tools/pmc_traffic.py from two
+    separate --pmc passes, FETCH_SIZE doubled per the gfx950 note), or None."""
     p = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
     try:
         with open(p) as f:
@@ -181,7 +184,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "kernel": "bb::step_kernel",
+                "kernel": "bb_step = bb::step_kernel + bb::escalate_kernel",
                 "kernel_avg_ms": round(kern_ms, 5),
                 "algo_bytes_per_launch": algo_bytes,
             },

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""BASELINE config 3 (full PPO on one MI355X): rollout + update timing.
+
+One PPO iteration at the reference hyper-parameters is T=128 rollout steps of
+N envs, then num_epochs x (T*N / batch) optimizer steps.  At N=65,536 that is
+40,960 optimizer steps, so the update is timed over ``--update-steps``
+minibatches and extrapolated (stated in the output).  FLOP accounting follows
+SURVEY.md §8(d): 113,049,856 FLOP per sample forward, x3 for forward+backward.
+
+Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd"), REPO]
+
+import torch  # noqa: E402
+
+FWD_FLOP = 113_049_856
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--rollout", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--epochs", type=int, default=10)
+    ap.add_argument("--update-steps", type=int, default=100)
+    ap.add_argument("--autocast", choices=["none", "bf16"], default="none")
+    args = ap.parse_args()
+
+    from agents import PPOAgent, PPOConfig
+    from training.trainer import DeviceRollout
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    agent = PPOAgent(PPOConfig(batch_size=args.batch, num_epochs=args.epochs), device=dev, sample_seed=1)
+    if args.autocast == "bf16":
+        agent.autocast_dtype = torch.bfloat16
+    agent.train()
+    roll = DeviceRollout(args.envs, 0, args.envs, 42, {}, args.rollout, dev)
+    roll.reset()
+    # warm-up: a short rollout + a few optimizer steps (kernels, MIOpen tuning)
+    roll_w = DeviceRollout(min(args.envs, 4096), 0, min(args.envs, 4096), 7, {}, 4, dev)
+    roll_w.reset()
+    roll_w.collect(agent)
+    agent.update(roll_w.buffer, agent.values_device(roll_w.x), batch_size=args.batch)
+    roll_w.close()
+    agent.values_device(roll.x)
+    torch.cuda.synchronize()
+
+    t0 = time.perf_counter()
+    roll.collect(agent)
+    last = agent.values_device(roll.x)
+    torch.cuda.synchronize()
+    t_roll = time.perf_counter() - t0
+
+    buf = roll.buffer
+    buf.compute_returns_and_advantages(last, 0.99, 0.95)
+    batches = buf.get_minibatches(args.batch)
+    done = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for x, m, a, lp, adv, ret in batches:
+        loss, _ = agent._minibatch_loss(x, m, a, lp, adv, ret)
+        agent._optimizer_step(loss)
+        done += 1
+        if done >= args.update_steps:
+            break
+    torch.cuda.synchronize()
+    t_upd_step = (time.perf_counter() - t0) / done
+
+    samples = args.envs * args.rollout
+    n_steps = args.epochs * -(-samples // args.batch)
+    t_update = t_upd_step * n_steps
+    t_iter = t_roll + t_update
+    roll_flops = samples * FWD_FLOP / t_roll
+    upd_flops = 3 * FWD_FLOP * args.batch / t_upd_step
+    print(json.dumps({
+        "workload": "BASELINE config 3: full PPO iteration on 1 MI355X", "envs": args.envs, "rollout_steps": args.rollout,
+        "batch": args.batch, "epochs": args.epochs, "compute_dtype": "bf16 autocast" if args.autocast == "bf16" else "fp32",
+        "rollout_s": round(t_roll, 4), "rollout_env_steps_per_s": round(samples / t_roll, 1),
+        "rollout_cnn_tflops": round(roll_flops / 1e12, 2),
+        "update_step_ms": round(t_upd_step * 1e3, 3), "update_steps_timed": done, "update_steps_total": n_steps,
+        "update_s_extrapolated": round(t_update, 2), "update_cnn_tflops": round(upd_flops / 1e12, 2),
+        "iteration_s": round(t_iter, 2), "ppo_env_steps_per_s": round(samples / t_iter, 1),
+    }))
+    roll.close()
+
+
+if __name__ == "__main__":
+    main()
