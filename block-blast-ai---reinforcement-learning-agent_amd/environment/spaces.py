@@ -14,6 +14,7 @@ try:  # pragma: no cover - depends on the image
     from gymnasium import spaces as _spaces
 
     Env = _gym.Env
+    Wrapper = _gym.Wrapper
     Box = _spaces.Box
     Discrete = _spaces.Discrete
     Dict = _spaces.Dict
@@ -26,6 +27,33 @@ except Exception:  # gymnasium absent
 
         def reset(self, seed=None, options=None):
             return None
+
+    class Wrapper(Env):  # minimal gym.Wrapper stand-in: delegate to the wrapped env
+        def __init__(self, env):
+            self.env = env
+            self.observation_space = env.observation_space
+            self.action_space = env.action_space
+
+        def step(self, action):
+            return self.env.step(action)
+
+        def reset(self, **kwargs):
+            return self.env.reset(**kwargs)
+
+        def render(self):
+            return self.env.render()
+
+        def close(self):
+            return self.env.close()
+
+        @property
+        def unwrapped(self):
+            return getattr(self.env, "unwrapped", self.env)
+
+        def __getattr__(self, name):
+            if name.startswith("_"):
+                raise AttributeError(name)
+            return getattr(self.env, name)
 
     class Box:
         def __init__(self, low, high, shape, dtype):
