@@ -26,7 +26,9 @@ struct bb_env {
   uint8_t* d_dtab = nullptr;
   JumpRow* d_jump = nullptr;
   void* slab = nullptr;
-  int lane_budget = 0;  // 0: every hand search runs wave-cooperatively (escalate_kernel)
+  int lane_budget = 16; // in-lane search budget before parking (BB_LANE_BUDGET; 0 = park every draw)
+  int pack_first = 8;   // escalate pass schedule (BB_PACK_FIRST / BB_PACK_NEXT, tuning only)
+  int pack_next = 32;
   int dbg = 0;
   uint64_t* dbg_out = nullptr;
   std::string err;
@@ -125,6 +127,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   e->cfg = *cfg;
   if (const char* s = getenv("BB_LANE_BUDGET")) e->lane_budget = atoi(s) > 0 ? atoi(s) : 0;
   if (const char* s = getenv("BB_DEBUG_MODE")) e->dbg = atoi(s);
+  if (const char* s = getenv("BB_PACK_FIRST")) e->pack_first = atoi(s) > 0 ? atoi(s) : 1;
+  if (const char* s = getenv("BB_PACK_NEXT")) e->pack_next = atoi(s) > 0 ? atoi(s) : 0;
   const size_t bytes = slab_bytes(num_envs);
   st = hipMalloc(&e->slab, bytes);
   if (st != hipSuccess) {
@@ -249,6 +253,8 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.center_tenth = env->cfg.center_bonus * 0.1;
   a.autoreset = env->autoreset;
   a.lane_budget = env->lane_budget;
+  a.pack_first = env->pack_first;
+  a.pack_next = env->pack_next;
   a.jump = env->d_jump;
   a.dbg = env->dbg;
   a.dbg_out = env->dbg_out;

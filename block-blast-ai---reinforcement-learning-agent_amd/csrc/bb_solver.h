@@ -325,12 +325,13 @@ __device__ __forceinline__ bool draw_attempt_jump(const Pcg& s0, const JumpRow* 
 
 __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& ids, int attempt,
                                               const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
-                                              int lane, uint32_t* stats = nullptr) {
+                                              int lane, int pack_first, int pack_next,
+                                              uint32_t* stats = nullptr) {
   const int attempt0 = attempt;
   // anchors of every piece on B: lane x holds piece x
   const uint64_t acache = lane < kPieces ? anchors_of(tbl[lane], B) : 0ull;
   uint32_t last_ids = ids;
-  int pack = 1;
+  int pack = pack_first < kPack ? pack_first : kPack;
 #pragma unroll 1
   while (attempt < kMaxAttempts) {
     // ---- draw a batch: lane k = attempt k --------------------------------
@@ -438,7 +439,8 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
     rng.buf = __shfl(e_after.buf, jl);
     rng.has = __shfl((int)e_after.has, jl) != 0;
     attempt += nb;
-    pack = pack * 2 < kPack ? pack * 2 : kPack;
+    pack = pack_next > 0 ? pack_next : pack * 2;
+    pack = pack < kPack ? pack : kPack;
   }
   ids = last_ids;  // 100 failures: the last hand is kept (engine.py:171-172)
   if (stats) stats[0] = (uint32_t)(attempt - attempt0);

@@ -45,8 +45,15 @@ def _case(rng, fill):
 
 
 @pytest.mark.parametrize("fill", [0.45, 0.6, 0.7, 0.8, 0.9, 0.95, -1.0])
-def test_crowded_board_hand_generation(cuda, fill):
+@pytest.mark.parametrize("pack", ["1,0", "32,32", "3,7"])
+def test_crowded_board_hand_generation(cuda, fill, pack, monkeypatch):
+    """pack = escalation pass schedule (first pass attempts, later passes;
+    0 = doubling): every schedule must give the same hands."""
     from runtime.device_env import DeviceEnvBatch
+
+    first, nxt = pack.split(",")
+    monkeypatch.setenv("BB_PACK_FIRST", first)
+    monkeypatch.setenv("BB_PACK_NEXT", nxt)
 
     n = 512
     rng = np.random.default_rng(int(fill * 100) + 1000)
