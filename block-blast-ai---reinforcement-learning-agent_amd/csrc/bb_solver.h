@@ -209,6 +209,19 @@ __device__ __forceinline__ bool line_then_fits(uint64_t B1, const PieceRow& firs
   return has_full_line(B2) && anchors_of(second, clear_full(B2)) != 0ull;
 }
 
+// Some row or column has at most 5 empty cells (>= 3 filled): a prerequisite
+// for any single placement to complete a line.
+__device__ __forceinline__ bool line_within_reach(uint64_t B) {
+  uint64_t x = B - ((B >> 1) & 0x5555555555555555ull);
+  x = (x & 0x3333333333333333ull) + ((x >> 2) & 0x3333333333333333ull);
+  x = (x + (x >> 4)) & 0x0F0F0F0F0F0F0F0Full;  // per-row popcounts, one byte each
+  if ((x + 0x7D7D7D7D7D7D7D7Dull) & 0x8080808080808080ull) return true;
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    if (__popcll(B & (kCol0 << c)) >= 3) return true;
+  return false;
+}
+
 __device__ __forceinline__ bool pair_slow(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint64_t A2,
                                           uint64_t A3) {
   // G2: b-anchors at which every c-anchor collides (order b then c); G3 mirror
@@ -217,7 +230,10 @@ __device__ __forceinline__ bool pair_slow(uint64_t B1, const PieceRow& pb, const
   pair_conflict_mask(pc, pb, m3lo, m3hi);
   uint64_t G2 = ~0ull, G3 = ~0ull;
   uint64_t it3 = A3, it2 = A2;  // G2 runs over c-anchors, G3 over b-anchors
-  while (it3 | it2) {
+  // Both G's decide the same question (is there a disjoint b/c placement
+  // pair?), so the loop stops as soon as EITHER side is exhausted: that side
+  // is exact and the other one's partial G only under-reports successes.
+  while (it3 && it2) {
     const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
     const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
     G2 = and_shifted(and_shifted(G2, r0, m2lo, m2hi), r1, m2lo, m2hi);
@@ -225,7 +241,10 @@ __device__ __forceinline__ bool pair_slow(uint64_t B1, const PieceRow& pb, const
     if ((A2 & ~G2) | (A3 & ~G3)) return true;
   }
   if ((A2 & ~G2) | (A3 & ~G3)) return true;
-  // every first placement blocks every second one: only a line clear helps
+  // every first placement blocks every second one: only a line clear helps,
+  // and no single piece (at most 5 cells across) completes a line that has
+  // more than 5 empty cells
+  if (!line_within_reach(B1)) return false;
   it2 = A2;
   it3 = A3;
   while (it2 | it3) {
