@@ -202,13 +202,6 @@ __device__ __forceinline__ uint64_t pop_high(uint64_t& x) {
 __device__ __forceinline__ uint64_t and_shifted(uint64_t G, uint64_t bit, uint64_t mlo, uint64_t mhi) {
   return bit ? G & hi_shl(mlo, mhi, __ffsll((unsigned long long)bit) - 1) : G;
 }
-__device__ __forceinline__ bool line_then_fits(uint64_t B1, const PieceRow& first, const PieceRow& second,
-                                               uint64_t bit) {
-  if (!bit) return false;
-  const uint64_t B2 = B1 | (first.shape << (__ffsll((unsigned long long)bit) - 1));
-  return has_full_line(B2) && anchors_of(second, clear_full(B2)) != 0ull;
-}
-
 // Some row or column has at most 5 empty cells (>= 3 filled): a prerequisite
 // for any single placement to complete a line.
 __device__ __forceinline__ bool line_within_reach(uint64_t B) {
@@ -222,39 +215,101 @@ __device__ __forceinline__ bool line_within_reach(uint64_t B) {
   return false;
 }
 
-__device__ __forceinline__ bool pair_slow(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint64_t A2,
-                                          uint64_t A3) {
-  // G2: b-anchors at which every c-anchor collides (order b then c); G3 mirror
+// Exact level-2 search of one slot, phase A (per lane): is there a disjoint
+// placement pair (no line clear needed)?  Written for ILP: the two G
+// accumulations run side by side and every anchor mask is consumed from both
+// ends per trip.  Both G's decide the same question, so the scan stops as
+// soon as EITHER side is exhausted: that side is exact, the other one's
+// partial G only under-reports successes.
+// Returns 1 (yes), 0 (no, and no first placement completes a line), 2 (no
+// disjoint pair: C2 / C3 receive the line-completing anchors of b / c, the
+// only first placements that can still make room for the other piece).
+__device__ __forceinline__ bool completes_line(uint64_t B1, const PieceRow& y, uint64_t bit) {
+  return bit && has_full_line(B1 | (y.shape << (__ffsll((unsigned long long)bit) - 1)));
+}
+
+__device__ __forceinline__ int pair_disjoint(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint64_t A2,
+                                             uint64_t A3, uint64_t& C2, uint64_t& C3) {
   uint64_t m2lo, m2hi, m3lo, m3hi;
   pair_conflict_mask(pb, pc, m2lo, m2hi);
   pair_conflict_mask(pc, pb, m3lo, m3hi);
   uint64_t G2 = ~0ull, G3 = ~0ull;
   uint64_t it3 = A3, it2 = A2;  // G2 runs over c-anchors, G3 over b-anchors
-  // Both G's decide the same question (is there a disjoint b/c placement
-  // pair?), so the loop stops as soon as EITHER side is exhausted: that side
-  // is exact and the other one's partial G only under-reports successes.
   while (it3 && it2) {
     const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
     const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
     G2 = and_shifted(and_shifted(G2, r0, m2lo, m2hi), r1, m2lo, m2hi);
     G3 = and_shifted(and_shifted(G3, q0, m3lo, m3hi), q1, m3lo, m3hi);
-    if ((A2 & ~G2) | (A3 & ~G3)) return true;
+    if ((A2 & ~G2) | (A3 & ~G3)) return 1;
   }
-  if ((A2 & ~G2) | (A3 & ~G3)) return true;
-  // every first placement blocks every second one: only a line clear helps,
-  // and no single piece (at most 5 cells across) completes a line that has
-  // more than 5 empty cells
-  if (!line_within_reach(B1)) return false;
+  if ((A2 & ~G2) | (A3 & ~G3)) return 1;
+  // no single piece (at most 5 cells across) completes a line with more
+  // than 5 empty cells
+  if (!line_within_reach(B1)) return 0;
+  C2 = 0ull;
+  C3 = 0ull;
   it2 = A2;
   it3 = A3;
   while (it2 | it3) {
     const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
     const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
-    if (line_then_fits(B1, pb, pc, q0) | line_then_fits(B1, pb, pc, q1) | line_then_fits(B1, pc, pb, r0) |
-        line_then_fits(B1, pc, pb, r1))
-      return true;
+    if (completes_line(B1, pb, q0)) C2 |= q0;
+    if (completes_line(B1, pb, q1)) C2 |= q1;
+    if (completes_line(B1, pc, r0)) C3 |= r0;
+    if (completes_line(B1, pc, r1)) C3 |= r1;
   }
-  return false;
+  return (C2 | C3) ? 2 : 0;
+}
+
+// Phase B (whole wave): every lane's line candidates -- its first-piece
+// anchors C2 (b first) and C3 (c first), all line-completing -- are
+// flattened into one task list and dealt out 64 at a time, so one lane with
+// many candidates no longer holds the wave.  Task: place the first piece,
+// clear, does the second piece fit?  Returns this lane's verdict.  All lanes call it
+// (uniform control flow); lanes without candidates pass C2 = C3 = 0.
+__device__ __forceinline__ bool line_phase_wave(uint64_t B1, uint32_t bi, uint32_t ci, uint64_t C2, uint64_t C3,
+                                                const PieceRow* tbl, int lane) {
+  const uint32_t n2 = (uint32_t)__popcll(C2);
+  const uint32_t cnt = n2 + (uint32_t)__popcll(C3);
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  const uint32_t off = incl - cnt;
+  const uint32_t total = (uint32_t)__shfl(incl, 63);
+  uint64_t won = 0ull;  // bit l: lane l's slot succeeded
+#pragma unroll 1
+  for (uint32_t base = 0; base < total; base += 64u) {
+    const uint32_t t = base + (uint32_t)lane;
+    int o = 0;  // owner: last lane with off <= t (and cnt > 0 in range)
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1) {
+      const int cand = o + step;
+      const uint32_t co = __shfl(off, cand < 64 ? cand : 63);
+      if (cand < 64 && co <= t) o = cand;
+    }
+    const uint64_t oB = __shfl(B1, o);
+    const uint64_t oC2 = __shfl(C2, o), oC3 = __shfl(C3, o);
+    const uint32_t oid = __shfl(bi | (ci << 8), o);
+    const uint32_t k = t - __shfl(off, o);
+    const uint32_t on2 = (uint32_t)__popcll(oC2);
+    bool hit = false;
+    if (t < total) {
+      const bool bfirst = k < on2;
+      const PieceRow& first = tbl[bfirst ? (oid & 0xFFu) : (oid >> 8)];
+      const PieceRow& second = tbl[bfirst ? (oid >> 8) : (oid & 0xFFu)];
+      const int pos = select_bit(bfirst ? oC2 : oC3, bfirst ? k : k - on2);
+      const uint64_t B2 = oB | (first.shape << pos);
+      hit = anchors_of(second, clear_full(B2)) != 0ull;  // candidates complete a line
+    }
+    uint64_t m = hit ? (1ull << o) : 0ull;
+#pragma unroll
+    for (int x = 1; x < 64; x <<= 1) m |= __shfl_xor(m, x);
+    won |= m;
+  }
+  return (won >> lane) & 1ull;
 }
 
 
@@ -437,7 +492,13 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
         const uint32_t sl = (uint32_t)(total - base < 64 ? total - base : 64);
         stats[3] = stats[3] > sl ? stats[3] : sl;
       }
-      if (needs && need) ok = pair_slow(B1, tbl[bi], tbl[ci], A2, A3);
+      if (needs) {
+        uint64_t C2 = 0ull, C3 = 0ull;
+        if (need) {
+          ok = pair_disjoint(B1, tbl[bi], tbl[ci], A2, A3, C2, C3) == 1;
+        }
+        if (__ballot((C2 | C3) != 0ull)) ok |= line_phase_wave(B1, bi, ci, C2, C3, tbl, lane);
+      }
       const uint64_t hit = __ballot(ok);
       if (hit) {
         const int jw = __shfl(j, __ffsll((unsigned long long)hit) - 1);
