@@ -178,8 +178,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
     delete e;
     return fail(nullptr, BB_ERR_HIP, m);
   }
-  if (e->dbg & 2) {
-    if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~2;
+  if (e->dbg & 6) {
+    if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~6;
     else (void)hipMemset(e->dbg_out, 0, n * 32);
   }
   *out = e;
@@ -397,7 +397,7 @@ int bb_set_state(bb_env* env, const bb_state_view* v) {
 
 int bb_debug_counters(bb_env* env, uint64_t* h_out) {
   if (!env || !h_out) return BB_ERR_ARG;
-  if (!env->dbg_out) return fail(env, BB_ERR_STATE, "bb_debug_counters: create with BB_DEBUG_MODE bit 1 set");
+  if (!env->dbg_out) return fail(env, BB_ERR_STATE, "bb_debug_counters: create with BB_DEBUG_MODE bit 1 or 2 set");
   DeviceGuard g(env->device);
   hipError_t st = hipDeviceSynchronize();
   if (st == hipSuccess) st = hipMemcpy(h_out, env->dbg_out, (size_t)env->n * 32, hipMemcpyDeviceToHost);

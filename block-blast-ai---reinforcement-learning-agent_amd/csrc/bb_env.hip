@@ -32,21 +32,50 @@
 namespace bb {
 
 constexpr int kStepBlock = 64;
-constexpr int kEscBlock = 256;
+#ifndef BB_ESC_BLOCK
+#define BB_ESC_BLOCK 256
+#endif
+constexpr int kEscBlock = BB_ESC_BLOCK;
 #ifndef BB_ESC_GROUP
 #define BB_ESC_GROUP 8
 #endif
 constexpr int kEscGroup = BB_ESC_GROUP;  // envs owned by one escalation wave
 
-struct Tables {
-  PieceRow row[kPieces];
-  uint8_t d[kPieces * kPieces];
-};
+constexpr int kDPad = (kPieces * kPieces + 15) / 16 * 16;  // |D| table padded to whole 16-byte vectors
 
+struct alignas(16) Tables {
+  PieceRow row[kPieces];
+  uint8_t d[kDPad];
+};
+static_assert(sizeof(PieceRow) % 16 == 0, "PieceRow staged as 16-byte vectors");
+
+// Global -> LDS copy of the piece rows and the |D| table as 16-byte vectors:
+// every load of a thread is issued before its first LDS store, so the
+// staging costs one memory latency (byte-wise copying cost ~22 serial ones).
+// The device buffers are padded (slab carving rounds to 256 bytes).
 __device__ __forceinline__ void stage_tables(Tables& t, const PieceRow* g_rows, const uint8_t* g_d) {
+  constexpr int kRowVec = kPieces * (int)sizeof(PieceRow) / 16;
+  constexpr int kTot = kRowVec + kDPad / 16;
+  constexpr int kPer = (kTot + 63) / 64;
+  const uint4* rs = reinterpret_cast<const uint4*>(g_rows);
+  const uint4* ds = reinterpret_cast<const uint4*>(g_d);
+  uint4* rd = reinterpret_cast<uint4*>(t.row);
+  uint4* dd = reinterpret_cast<uint4*>(t.d);
   const int tid = threadIdx.x;
-  if (tid < kPieces) t.row[tid] = g_rows[tid];
-  for (int i = tid; i < kPieces * kPieces; i += blockDim.x) t.d[i] = g_d[i];
+  uint4 v[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int idx = tid + k * (int)blockDim.x;
+    if (idx < kTot) v[k] = idx < kRowVec ? rs[idx] : ds[idx - kRowVec];
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int idx = tid + k * (int)blockDim.x;
+    if (idx < kTot) {
+      if (idx < kRowVec) rd[idx] = v[k];
+      else dd[idx - kRowVec] = v[k];
+    }
+  }
   __syncthreads();
 }
 
@@ -245,31 +274,37 @@ __global__ void __launch_bounds__(kStepBlock) reset_kernel(EnvDev e, const Piece
 __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                           const int32_t* __restrict__ actions, StepArgs a) {
   __shared__ Tables t;
-  stage_tables(t, g_rows, g_d);
+  const bool prof = (a.dbg & 4) != 0;  // diagnostics: phase timestamps
+  const uint64_t T0 = prof ? __builtin_amdgcn_s_memtime() : 0;
   const int i = blockIdx.x * kStepBlock + threadIdx.x;
-  if (i >= e.n) return;
-
-  // ---- every column up front: one memory round trip ----------------------
+  const bool live = i < e.n;
+  // ---- every column up front (in flight while the tables are staged) ------
   StepCtx s;
-  s.i = i;
-  const int act = actions[i];
-  s.B = e.board[i];
-  s.hand = e.hand[i];
-  s.score = e.score[i];
-  s.combo = e.combo[i];
-  s.max_combo = e.max_combo[i];
-  s.moves = e.moves[i];
-  s.lines_tot = e.lines[i];
-  s.blocks = e.blocks[i];
-  s.prev = e.prev[i];
-  s.rng.hi = e.rng_hi[i];
-  s.rng.lo = e.rng_lo[i];
-  s.rng.buf = e.rng_buf[i];
-  s.rng.inc_hi = e.inc_hi[i];
-  s.rng.inc_lo = e.inc_lo[i];
-  s.seed_hi = e.seed_hi[i];
-  s.seed_lo = e.seed_lo[i];
-  s.has_seed = e.has_seed[i] != 0;
+  int act = -1;
+  if (live) {
+    s.i = i;
+    act = actions[i];
+    s.B = e.board[i];
+    s.hand = e.hand[i];
+    s.score = e.score[i];
+    s.combo = e.combo[i];
+    s.max_combo = e.max_combo[i];
+    s.moves = e.moves[i];
+    s.lines_tot = e.lines[i];
+    s.blocks = e.blocks[i];
+    s.prev = e.prev[i];
+    s.rng.hi = e.rng_hi[i];
+    s.rng.lo = e.rng_lo[i];
+    s.rng.buf = e.rng_buf[i];
+    s.rng.inc_hi = e.inc_hi[i];
+    s.rng.inc_lo = e.inc_lo[i];
+    s.seed_hi = e.seed_hi[i];
+    s.seed_lo = e.seed_lo[i];
+    s.has_seed = e.has_seed[i] != 0;
+  }
+  stage_tables(t, g_rows, g_d);
+  const uint64_t T1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  if (!live) return;
   s.rng.has = hand_has32(s.hand);
   s.drew = false;
   s.nblk = 0;
@@ -288,6 +323,8 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
     valid = ((pr.anchors >> cell) & 1ull) && ((pr.shape << cell) & s.B) == 0;
   }
   s.valid = valid;
+  const uint64_t T2 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t T3 = T2;
 
   if (valid) {
     // ---- make_move: engine.py:406-429 ------------------------------------
@@ -311,6 +348,7 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
     }
     s.score += s.gained;
     uint32_t ids = s.hand & 0x3FFFFu;
+    if (prof) T3 = __builtin_amdgcn_s_memtime();
     if (used == 7u) {
       // ---- all three used -> new hand (engine.py:432-437) ---------------
       used = 0;
@@ -350,13 +388,24 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
         e.blocks[i] = s.blocks;
         e.pscratch[i] = pack_pending(attempt, s.nblk, s.lines, s.cm, s.gained);
         e.pend[i] = 1;
+        if (prof) {
+          const uint64_t T4 = __builtin_amdgcn_s_memtime();
+          a.dbg_out[4 * i + 0] = (T1 - T0) | ((T2 - T1) << 16) | ((T3 - T2) << 32) | ((T4 - T3) << 48);
+          a.dbg_out[4 * i + 1] = 1;
+        }
         return;
       }
     } else {
       s.hand = ids | (used << 18) | (s.hand & (1u << 22));
     }
   }
+  const uint64_t T4 = prof ? __builtin_amdgcn_s_memtime() : 0;
   finalize(t, e, s, a);
+  if (prof) {
+    const uint64_t T5 = __builtin_amdgcn_s_memtime();
+    a.dbg_out[4 * i + 0] = (T1 - T0) | ((T2 - T1) << 16) | ((T3 - T2) << 32) | ((T4 - T3) << 48);
+    a.dbg_out[4 * i + 1] = 2 | ((T5 - T4) << 16) | ((uint64_t)s.drew << 8);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -365,15 +414,14 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
 __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a) {
   __shared__ Tables t;
-  stage_tables(t, g_rows, g_d);
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * kEscBlock + threadIdx.x) >> 6;
   const int base = wave * kEscGroup;
   const int mine = base + lane;
   const bool flagged = lane < kEscGroup && mine < e.n && e.pend[mine] != 0;
   const uint64_t parked = __ballot(flagged);
-  if (!parked) return;
-  // owner lane k holds env base+k: all of its columns in one round trip
+  // owner lane k holds env base+k: all of its columns in one round trip,
+  // in flight while the tables are staged (every thread stages its share)
   StepCtx s;
   uint64_t pr = 0;
   if (flagged) {
@@ -404,6 +452,8 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
     s.cm = (int)((pr >> 24) & 0xFFu);
     s.gained = (int64_t)(uint32_t)(pr >> 32);
   }
+  stage_tables(t, g_rows, g_d);
+  if (!parked) return;
   // one parked env at a time, searched by the whole wave (register broadcast)
   uint32_t my_ids = 0;
   uint64_t it = parked;
