@@ -28,6 +28,7 @@ def main():
     env.random_actions(mb, act[0], step=0)
     buf = np.zeros((n, 4), dtype=np.uint64)
     lane_ok, lane_park, esc = [], [], []
+    wave_tot = []
     draws = parked = 0
     for t in range(warm + steps):
         env.step(act[t & 1], next_action=act[(t + 1) & 1], policy_step=t + 1)
@@ -41,10 +42,14 @@ def main():
         lane_ok.extend(buf[lane & ~pk, 0].astype(np.int64).tolist())
         lane_park.extend(buf[lane & pk, 0].astype(np.int64).tolist())
         esc.extend(buf[pk, 2].astype(np.int64).tolist())
+        e2 = np.where(pk, buf[:, 2].astype(np.int64), 0)
+        wt = e2.reshape(-1, 8).sum(1)
+        wave_tot.append(int(wt.max()))
     pc = lambda v: {p: float(np.percentile(v, p)) for p in (50, 90, 99, 100)} if len(v) else None  # noqa: E731
     print(json.dumps({"budget": os.environ.get("BB_LANE_BUDGET", "0"), "draws_per_step": draws / steps,
                       "parked_per_step": parked / steps, "lane_settled_cycles": pc(lane_ok),
-                      "lane_parked_cycles": pc(lane_park), "escalate_cycles": pc(esc)}))
+                      "lane_parked_cycles": pc(lane_park), "escalate_cycles": pc(esc),
+                      "escalate_wave_max_per_step": pc(wave_tot)}))
 
 
 if __name__ == "__main__":
