@@ -100,10 +100,18 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BB_BENCH_SHARE_GPU=1 (tests only): every rank on cuda:0 over gloo, to
+    # exercise the multi-rank path on a one-GPU box; the numbers are not a bench
+    share = os.environ.get("BB_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -146,7 +154,7 @@ def main() -> None:
     el = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # average bb_step (both kernels + their launch gap)
     if world > 1:
-        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([el, kern_ms], dtype=torch.float64, device="cpu" if share else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
 
