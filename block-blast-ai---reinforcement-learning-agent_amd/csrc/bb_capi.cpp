@@ -27,6 +27,7 @@ struct bb_env {
   JumpRow* d_jump = nullptr;
   void* slab = nullptr;
   int lane_budget = 16; // in-lane search budget before parking (BB_LANE_BUDGET; 0 = park every draw)
+  int lane_quick = 2;   // in-lane test of 2 fixed slots (BB_LANE_QUICK; 0 = budget search instead)
   int pack_first = 8;   // escalate pass schedule (BB_PACK_FIRST / BB_PACK_NEXT, tuning only)
   int pack_next = 32;
   int dbg = 0;
@@ -127,6 +128,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   e->cfg = *cfg;
   if (const char* s = getenv("BB_LANE_BUDGET")) e->lane_budget = atoi(s) > 0 ? atoi(s) : 0;
   if (const char* s = getenv("BB_DEBUG_MODE")) e->dbg = atoi(s);
+  if (const char* s = getenv("BB_LANE_QUICK")) e->lane_quick = atoi(s) > 0 ? atoi(s) : 0;
+  if (getenv("BB_LANE_BUDGET") && !getenv("BB_LANE_QUICK")) e->lane_quick = 0;  // explicit budget mode
   if (const char* s = getenv("BB_PACK_FIRST")) e->pack_first = atoi(s) > 0 ? atoi(s) : 1;
   if (const char* s = getenv("BB_PACK_NEXT")) e->pack_next = atoi(s) > 0 ? atoi(s) : 0;
   const size_t bytes = slab_bytes(num_envs);
@@ -253,6 +256,7 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.center_tenth = env->cfg.center_bonus * 0.1;
   a.autoreset = env->autoreset;
   a.lane_budget = env->lane_budget;
+  a.lane_quick = env->lane_quick;
   a.pack_first = env->pack_first;
   a.pack_next = env->pack_next;
   a.jump = env->d_jump;

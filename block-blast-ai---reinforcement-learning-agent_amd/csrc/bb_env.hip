@@ -360,8 +360,10 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
         ids |= draw_piece(s.rng) << 6;
         ids |= draw_piece(s.rng) << 12;
         done = true;
+      } else if (a.lane_quick > 0) {
+        done = quick_hand(s.B, s.rng, ids, t.row, t.d, a.lane_quick);
       } else if (a.lane_budget <= 0) {
-        done = false;  // default: every search runs wave-cooperatively in escalate_kernel
+        done = false;  // every search runs wave-cooperatively in escalate_kernel
       } else {
         const uint64_t c0 = (a.dbg & 2) ? __builtin_amdgcn_s_memtime() : 0;
         done = gen_hand_lane(s.B, s.rng, ids, attempt, t.row, t.d, a.lane_budget);

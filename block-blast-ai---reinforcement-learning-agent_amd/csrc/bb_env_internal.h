@@ -41,6 +41,7 @@ struct StepArgs {
   double center_tenth;  // reward_config['center_bonus'] * 0.1 (block_blast_env.py:190)
   int autoreset;
   int lane_budget;      // per-lane solver budget before wave escalation
+  int lane_quick;       // > 0: in-lane test of this many fixed slots instead of the budget search
   int pack_first;       // attempts drawn in the first wave pass (>= 1)
   int pack_next;        // attempts per later pass (0: double each pass)
   const JumpRow* jump;  // PCG64 jump-ahead table [kJumpMax + 1]

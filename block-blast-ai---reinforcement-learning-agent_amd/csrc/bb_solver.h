@@ -183,6 +183,40 @@ __device__ __forceinline__ int pair_quick(uint64_t B1, const PieceRow& pb, const
   return 2;
 }
 
+// In-lane quick test of the first attempt (step_kernel): draw its three
+// pieces and test up to `slots` fixed level-1 slots -- first piece f = k mod 3
+// at its lowest (k < 3) or highest anchor -- with pair_quick.  Straight-line
+// work, no budget loop.  Settles only on an accept (an exact success); else
+// rolls the stream back so the wave search redraws the attempt.
+__device__ __forceinline__ bool quick_hand(uint64_t B, Pcg& rng, uint32_t& ids, const PieceRow* tbl,
+                                           const uint8_t* dtab, int slots) {
+  const Pcg save = rng;
+  const uint32_t x0 = draw_piece(rng);
+  const uint32_t x1 = draw_piece(rng);
+  const uint32_t x2 = draw_piece(rng);
+  ids = x0 | (x1 << 6) | (x2 << 12);
+  uint64_t A[3];
+  A[0] = anchors_of(tbl[x0], B);
+  A[1] = anchors_of(tbl[x1], B);
+  A[2] = anchors_of(tbl[x2], B);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    if (k >= slots) break;
+    const int f = k % 3;
+    const uint64_t Af = A[f];
+    if (!Af) continue;
+    const uint32_t fi = f == 0 ? x0 : (f == 1 ? x1 : x2);
+    const uint32_t bi = f == 0 ? x1 : x0;
+    const uint32_t ci = f == 2 ? x1 : x2;
+    const int p = k < 3 ? __ffsll((unsigned long long)Af) - 1 : 63 - __clzll((long long)Af);
+    const uint64_t B1 = clear_full(B | (tbl[fi].shape << p));
+    uint64_t A2, A3;
+    if (pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3) == 1) return true;
+  }
+  rng = save;
+  return false;
+}
+
 // Exact level-2 search of one slot (both orders), written for ILP: the two
 // orders' G accumulations run side by side and every anchor mask is consumed
 // from both ends (lowest and highest set bit) per iteration, so four

@@ -81,13 +81,16 @@ def test_vec_env_bit_exact_custom_rewards(cuda):
     _run_parity(n=64, steps=120, seed=7, p_invalid=0.05, reward_config=rc, act_seed=3)
 
 
-@pytest.mark.parametrize("budget", ["0", "1", "64", "1000000000"])
+@pytest.mark.parametrize("budget", ["0", "1", "16", "64", "1000000000", "q1", "q3", "q6"])
 def test_vec_env_solver_paths(cuda, monkeypatch, budget):
-    """Budget 0 (default) sends every hand search to the wave-cooperative
-    escalation kernel, 1 / 64 escalate after a partial in-lane search, a huge
-    budget keeps every search inside its lane.  All must reproduce the oracle
-    bit for bit."""
-    monkeypatch.setenv("BB_LANE_BUDGET", budget)
+    """Budget 0 sends every hand search to the wave-cooperative escalation
+    kernel, 1 / 16 / 64 escalate after a partial in-lane search, a huge budget
+    keeps every search inside its lane, qK tests K fixed slots in-lane.  All
+    must reproduce the oracle bit for bit."""
+    if budget.startswith("q"):
+        monkeypatch.setenv("BB_LANE_QUICK", budget[1:])
+    else:
+        monkeypatch.setenv("BB_LANE_BUDGET", budget)
     terms = _run_parity(n=64, steps=120, seed=4242, p_invalid=0.05, act_seed=9)
     assert terms > 20
 
