@@ -181,8 +181,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
     delete e;
     return fail(nullptr, BB_ERR_HIP, m);
   }
-  if (e->dbg & 6) {
-    if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~6;
+  if (e->dbg & 14) {
+    if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~14;
     else (void)hipMemset(e->dbg_out, 0, n * 32);
   }
   *out = e;

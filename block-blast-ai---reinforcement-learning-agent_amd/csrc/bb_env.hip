@@ -156,8 +156,11 @@ __device__ __forceinline__ void store_reset(const EnvDev& e, int i, const Pcg& r
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepCtx& s, const StepArgs& a) {
   const int i = s.i;
+  const bool fprof = (a.dbg & 8) != 0;  // diagnostics: finalize sub-phase timestamps
+  const uint64_t F0 = fprof ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t m[3];
   masks_of(t, s.B, s.hand, m);
+  const uint64_t F1 = fprof ? __builtin_amdgcn_s_memtime() : 0;
   double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
   bool term = false;
   int holes = 0, center = 0;
@@ -186,6 +189,7 @@ __device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepC
     holes = count_holes(s.B);
   }
 
+  const uint64_t F2 = fprof ? __builtin_amdgcn_s_memtime() : 0;
   if (a.info) {
     bb_info inf;
     inf.score = s.score;
@@ -210,6 +214,7 @@ __device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepC
   if (a.reward_f64) a.reward_f64[i] = rew;
   if (a.lines) a.lines[i] = (uint8_t)s.lines;
 
+  const uint64_t F3 = fprof ? __builtin_amdgcn_s_memtime() : 0;
   if (term && a.autoreset) {
     // wrappers.py:97-102: env.reset() with the stored seed_value
     uint64_t B;
@@ -235,6 +240,7 @@ __device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepC
     e.mask[3 * i + 1] = m[1];
     e.mask[3 * i + 2] = m[2];
   }
+  const uint64_t F4 = fprof ? __builtin_amdgcn_s_memtime() : 0;
   if (a.mask_out) {
     a.mask_out[3 * i + 0] = m[0];
     a.mask_out[3 * i + 1] = m[1];
@@ -242,6 +248,11 @@ __device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepC
   }
   if (a.next_action) {
     a.next_action[i] = random_policy(m[0], m[1], m[2], a.policy_seed, a.env_offset + (uint64_t)i, a.policy_step);
+  }
+  if (fprof) {
+    const uint64_t F5 = __builtin_amdgcn_s_memtime();
+    a.dbg_out[4 * i + 2] = (F1 - F0) | ((F2 - F1) << 16) | ((F3 - F2) << 32) | ((F4 - F3) << 48);
+    a.dbg_out[4 * i + 3] = (F5 - F4) | ((uint64_t)(term ? 1 : 0) << 32);
   }
 }
 
