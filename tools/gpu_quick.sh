@@ -18,3 +18,7 @@ if [ "${PROF:-1}" = 1 ]; then
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1 || exit 1
   grep "bb::" "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG/run_kernel_stats.csv" | cut -c1-40,100-200
 fi
+for kv in ${EXTRA:-}; do
+  timeout -k 10 120 env $kv python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/bench_${TAG}_x.json" 2>/dev/null || exit 1
+  python -c "import json;d=json.load(open('$GRAFT_REPO_ROOT/gpurun_out/bench_${TAG}_x.json'));print('bench $kv', d['value'], d['roofline']['kernel_avg_ms'])"
+done
