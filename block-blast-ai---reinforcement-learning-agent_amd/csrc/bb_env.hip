@@ -484,13 +484,14 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
     const int watt = __shfl((int)(pr & 0xFFu), k);
     uint32_t ids = 0;
     const uint64_t c0 = (a.dbg & 2) ? __builtin_amdgcn_s_memtime() : 0;
-    uint32_t st[4] = {0, 0, 0, 0};
+    uint32_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     gen_hand_wave(wB, w, ids, watt, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, (a.dbg & 2) ? st : nullptr);
     if ((a.dbg & 2) && lane == 0) {
       a.dbg_out[4 * (base + k) + 2] = __builtin_amdgcn_s_memtime() - c0;
       a.dbg_out[4 * (base + k) + 1] = (uint64_t)st[0] | ((uint64_t)st[1] << 16) | ((uint64_t)st[2] << 32) |
                                       ((uint64_t)st[3] << 48);
-      a.dbg_out[4 * (base + k) + 3] = wB;
+      a.dbg_out[4 * (base + k) + 0] = (uint64_t)st[4] | ((uint64_t)st[5] << 32);
+      a.dbg_out[4 * (base + k) + 3] = (uint64_t)st[6] | ((uint64_t)st[7] << 32);
     }
     if (lane == k) {
       s.rng = w;

@@ -264,26 +264,33 @@ __device__ __forceinline__ bool completes_line(uint64_t B1, const PieceRow& y, u
 
 __device__ __forceinline__ int pair_disjoint(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint64_t A2,
                                              uint64_t A3, uint64_t& C2, uint64_t& C3) {
-  uint64_t m2lo, m2hi, m3lo, m3hi;
-  pair_conflict_mask(pb, pc, m2lo, m2hi);
-  pair_conflict_mask(pc, pb, m3lo, m3hi);
-  uint64_t G2 = ~0ull, G3 = ~0ull;
-  uint64_t it3 = A3, it2 = A2;  // G2 runs over c-anchors, G3 over b-anchors
-  while (it3 && it2) {
-    const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
-    const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
-    G2 = and_shifted(and_shifted(G2, r0, m2lo, m2hi), r1, m2lo, m2hi);
-    G3 = and_shifted(and_shifted(G3, q0, m3lo, m3hi), q1, m3lo, m3hi);
-    if ((A2 & ~G2) | (A3 & ~G3)) return 1;
+  // Only the smaller anchor set is scanned (four anchors per trip, two from
+  // each end): G = anchors of the OTHER piece that collide with every
+  // scanned placement; any other-piece anchor outside G gives a disjoint
+  // pair.  G only shrinks, so a hit found early is final.
+  const bool scan3 = __popcll(A3) <= __popcll(A2);
+  const PieceRow& other = scan3 ? pb : pc;  // piece whose anchors G collects
+  const PieceRow& scanned = scan3 ? pc : pb;
+  const uint64_t Aother = scan3 ? A2 : A3;
+  uint64_t mlo, mhi;
+  pair_conflict_mask(other, scanned, mlo, mhi);
+  uint64_t G = ~0ull;
+  uint64_t it = scan3 ? A3 : A2;
+  while (it) {
+    const uint64_t r0 = pop_low(it), r1 = pop_high(it);
+    const uint64_t r2 = pop_low(it), r3 = pop_high(it);
+    G = and_shifted(and_shifted(G, r0, mlo, mhi), r1, mlo, mhi);
+    G = and_shifted(and_shifted(G, r2, mlo, mhi), r3, mlo, mhi);
+    if (Aother & ~G) return 1;
   }
-  if ((A2 & ~G2) | (A3 & ~G3)) return 1;
+  if (!(A2 && A3)) G = ~0ull;  // a piece with no anchor: no disjoint pair
+  if (Aother & ~G) return 1;
   // no single piece (at most 5 cells across) completes a line with more
   // than 5 empty cells
   if (!line_within_reach(B1)) return 0;
   C2 = 0ull;
   C3 = 0ull;
-  it2 = A2;
-  it3 = A3;
+  uint64_t it2 = A2, it3 = A3;
   while (it2 | it3) {
     const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
     const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
@@ -476,6 +483,7 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
     // ---- test the batch: passes of 64 slots ------------------------------
 #pragma unroll 1
     for (int base = 0; base < total; base += 64) {
+      const uint64_t tq0 = stats ? __builtin_amdgcn_s_memtime() : 0;
       const int slot = base + lane;
       int j = 0;  // last packed attempt with e_off <= slot
 #pragma unroll
@@ -526,12 +534,24 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
         const uint32_t sl = (uint32_t)(total - base < 64 ? total - base : 64);
         stats[3] = stats[3] > sl ? stats[3] : sl;
       }
+      const uint64_t tq1 = stats ? __builtin_amdgcn_s_memtime() : 0;
+      if (stats) stats[4] += (uint32_t)(tq1 - tq0);
       if (needs) {
         uint64_t C2 = 0ull, C3 = 0ull;
         if (need) {
           ok = pair_disjoint(B1, tbl[bi], tbl[ci], A2, A3, C2, C3) == 1;
         }
+        const uint64_t tq2 = stats ? __builtin_amdgcn_s_memtime() : 0;
         if (__ballot((C2 | C3) != 0ull)) ok |= line_phase_wave(B1, bi, ci, C2, C3, tbl, lane);
+        if (stats) {
+          const uint64_t tq3 = __builtin_amdgcn_s_memtime();
+          stats[5] += (uint32_t)(tq2 - tq1);
+          stats[6] += (uint32_t)(tq3 - tq2);
+          uint32_t nt = (uint32_t)(__popcll(C2) + __popcll(C3));
+#pragma unroll
+          for (int x = 1; x < 64; x <<= 1) nt += __shfl_xor(nt, x);
+          stats[7] += nt;
+        }
       }
       const uint64_t hit = __ballot(ok);
       if (hit) {

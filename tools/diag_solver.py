@@ -46,10 +46,13 @@ def main():
         passes = ((f >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.int64)
         slow = ((f >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64)
         slots = (f >> np.uint64(48)).astype(np.int64)
+        w0 = buf[idx, 0]; w3 = buf[idx, 3]
+        quick_c = (w0 & np.uint64(0xFFFFFFFF)).astype(np.int64); disj_c = (w0 >> np.uint64(32)).astype(np.int64)
+        line_c = (w3 & np.uint64(0xFFFFFFFF)).astype(np.int64); line_t = (w3 >> np.uint64(32)).astype(np.int64)
         per_step.append((t, int(idx.size), int(cyc.max())))
         for k in range(idx.size):
-            rows.append((int(cyc[k]), int(att[k]), int(passes[k]), int(slow[k]), int(slots[k]), int(buf[idx[k], 3]), t,
-                         int(idx[k])))
+            rows.append((int(cyc[k]), int(att[k]), int(passes[k]), int(slow[k]), int(slots[k]), int(quick_c[k]), t,
+                         int(idx[k]), int(disj_c[k]), int(line_c[k]), int(line_t[k])))
     a = np.array([r[:5] for r in rows], dtype=np.int64)
     q = lambda v, p: float(np.percentile(v, p))  # noqa: E731
     out = {
@@ -61,9 +64,11 @@ def main():
         "frac_any_slow": float((a[:, 3] > 0).mean()),
         "cycles_by_slow_passes": {int(s): float(a[a[:, 3] == s, 0].mean()) for s in range(0, 6) if (a[:, 3] == s).any()},
         "per_step(t,n,max_cycles)": per_step[:12],
-        "worst": [dict(zip(("cycles", "attempts", "passes", "slow", "max_slots", "board", "step", "env"),
-                           r[:5] + (hex(r[5]),) + r[6:]))
+        "worst": [dict(zip(("cycles", "attempts", "passes", "slow", "max_slots", "quick_cyc", "step", "env",
+                            "disjoint_cyc", "line_cyc", "line_tasks"), r))
                   for r in sorted(rows, key=lambda r: -r[0])[:15]],
+        "totals_cycles": {"all": int(sum(r[0] for r in rows)), "quick": int(sum(r[5] for r in rows)),
+                          "disjoint": int(sum(r[8] for r in rows)), "line": int(sum(r[9] for r in rows))},
     }
     print(json.dumps(out, indent=1))
 
