@@ -290,14 +290,22 @@ __device__ __forceinline__ int pair_disjoint(uint64_t B1, const PieceRow& pb, co
   if (!line_within_reach(B1)) return 0;
   C2 = 0ull;
   C3 = 0ull;
-  uint64_t it2 = A2, it3 = A3;
-  while (it2 | it3) {
-    const uint64_t q0 = pop_low(it2), q1 = pop_high(it2);
-    const uint64_t r0 = pop_low(it3), r1 = pop_high(it3);
+  // four anchors per trip, each piece's set on its own (often one is empty)
+  uint64_t it2 = A2;
+  while (it2) {
+    const uint64_t q0 = pop_low(it2), q1 = pop_high(it2), q2 = pop_low(it2), q3 = pop_high(it2);
     if (completes_line(B1, pb, q0)) C2 |= q0;
     if (completes_line(B1, pb, q1)) C2 |= q1;
+    if (completes_line(B1, pb, q2)) C2 |= q2;
+    if (completes_line(B1, pb, q3)) C2 |= q3;
+  }
+  uint64_t it3 = A3;
+  while (it3) {
+    const uint64_t r0 = pop_low(it3), r1 = pop_high(it3), r2 = pop_low(it3), r3 = pop_high(it3);
     if (completes_line(B1, pc, r0)) C3 |= r0;
     if (completes_line(B1, pc, r1)) C3 |= r1;
+    if (completes_line(B1, pc, r2)) C3 |= r2;
+    if (completes_line(B1, pc, r3)) C3 |= r3;
   }
   return (C2 | C3) ? 2 : 0;
 }

@@ -48,7 +48,8 @@ def main():
         slots = (f >> np.uint64(48)).astype(np.int64)
         w0 = buf[idx, 0]; w3 = buf[idx, 3]
         quick_c = (w0 & np.uint64(0xFFFFFFFF)).astype(np.int64); disj_c = (w0 >> np.uint64(32)).astype(np.int64)
-        line_c = (w3 & np.uint64(0xFFFFFFFF)).astype(np.int64); line_t = (w3 >> np.uint64(32)).astype(np.int64)
+        line_c = (w3 & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        line_t = (w3 >> np.uint64(32)).astype(np.int64)
         per_step.append((t, int(idx.size), int(cyc.max())))
         for k in range(idx.size):
             rows.append((int(cyc[k]), int(att[k]), int(passes[k]), int(slow[k]), int(slots[k]), int(quick_c[k]), t,
