@@ -31,7 +31,10 @@
 
 namespace bb {
 
-constexpr int kStepBlock = 64;
+#ifndef BB_STEP_BLOCK
+#define BB_STEP_BLOCK 128
+#endif
+constexpr int kStepBlock = BB_STEP_BLOCK;
 #ifndef BB_ESC_BLOCK
 #define BB_ESC_BLOCK 256
 #endif
