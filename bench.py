@@ -92,6 +92,9 @@ def main() -> None:
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--mode", choices=("step", "rollout"), default="step",
+                    help="step: one bb_step launch per env-step; rollout: bb_rollout, T fused steps per launch")
+    ap.add_argument("--rollout-len", type=int, default=50, help="T, env-steps per bb_rollout launch")
     args = ap.parse_args()
 
     import torch
@@ -127,14 +130,33 @@ def main() -> None:
     env.random_actions(mbits, act[0], seed=POLICY_SEED, step=0)
 
     step_idx = [0]
+    T = max(1, args.rollout_len)
+    if args.mode == "rollout":
+        # per-step outputs of one launch, [T][N] (rewritten by every launch)
+        r_rew = torch.zeros((T, n), dtype=torch.float32, device=dev)
+        r_term = torch.zeros((T, n), dtype=torch.uint8, device=dev)
+        r_lines = torch.zeros((T, n), dtype=torch.uint8, device=dev)
+        r_act = torch.zeros((T, n), dtype=torch.int32, device=dev)
+        r_mask = torch.zeros((T, n, 3), dtype=torch.int64, device=dev)
 
-    def one_step():
+    def one_step(k=1):
         t = step_idx[0]
-        env.step(act[t & 1], next_action=act[(t + 1) & 1], policy_seed=POLICY_SEED, policy_step=t + 1)
-        step_idx[0] = t + 1
+        if args.mode == "step":
+            for j in range(k):
+                env.step(act[(t + j) & 1], next_action=act[(t + j + 1) & 1], policy_seed=POLICY_SEED,
+                         policy_step=t + j + 1)
+            step_idx[0] = t + k
+            return
+        done = 0
+        while done < k:  # T steps per launch, the action double-buffer flips once per launch
+            c = min(T, k - done)
+            env.rollout(c, act[0], r_rew, r_term, lines=r_lines, actions_out=r_act, mask_out=r_mask,
+                        next_action=act[1], policy_seed=POLICY_SEED, policy_step0=t + done)
+            act.reverse()
+            done += c
+        step_idx[0] = t + k
 
-    for _ in range(args.warmup):
-        one_step()
+    one_step(args.warmup)
 
     # HIP events on the launch stream (torch's current stream) bracket the
     # timed region; no event between steps (each timing event is a queue
@@ -145,8 +167,7 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.steps):
-        one_step()
+    one_step(args.steps)
     ev1.record()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -159,7 +180,8 @@ def main() -> None:
         el, kern_ms = float(t[0]), float(t[1])
 
     # sanity: every sampled action was legal -> no -10 rewards in the last step
-    assert bool((env.reward != -10.0).all()), "random policy produced an illegal action"
+    last_rew = env.reward if args.mode == "step" else r_rew
+    assert bool((last_rew != -10.0).all()), "random policy produced an illegal action"
 
     total_env_steps = n * world * args.steps
     value = total_env_steps / el
@@ -194,7 +216,8 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "kernel": "bb_step = bb::step_kernel + bb::escalate_kernel",
+                "kernel": ("bb_step = bb::step_kernel + bb::escalate_kernel" if args.mode == "step" else
+                           f"bb_rollout = bb::rollout_kernel, {T} env-steps per launch (time per env-step)"),
                 "kernel_avg_ms": round(kern_ms, 5),
                 "algo_bytes_per_launch": algo_bytes,
             },

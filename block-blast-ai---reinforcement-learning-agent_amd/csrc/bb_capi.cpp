@@ -94,6 +94,22 @@ size_t slab_bytes(int n) {
   return b;
 }
 
+// StepArgs fields that come from the handle (reward config, solver schedule).
+StepArgs base_args(const bb_env* env) {
+  StepArgs a{};
+  a.cfg = env->cfg;
+  a.center_tenth = env->cfg.center_bonus * 0.1;
+  a.autoreset = env->autoreset;
+  a.lane_budget = env->lane_budget;
+  a.lane_quick = env->lane_quick;
+  a.pack_first = env->pack_first;
+  a.pack_next = env->pack_next;
+  a.jump = env->d_jump;
+  a.dbg = env->dbg;
+  a.dbg_out = env->dbg_out;
+  return a;
+}
+
 }  // namespace
 
 extern "C" {
@@ -251,17 +267,7 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   if (!env) return BB_ERR_ARG;
   if (!d_actions || !out || !out->reward || !out->terminated)
     return fail(env, BB_ERR_ARG, "bb_step: actions, reward and terminated are required");
-  StepArgs a;
-  a.cfg = env->cfg;
-  a.center_tenth = env->cfg.center_bonus * 0.1;
-  a.autoreset = env->autoreset;
-  a.lane_budget = env->lane_budget;
-  a.lane_quick = env->lane_quick;
-  a.pack_first = env->pack_first;
-  a.pack_next = env->pack_next;
-  a.jump = env->d_jump;
-  a.dbg = env->dbg;
-  a.dbg_out = env->dbg_out;
+  StepArgs a = base_args(env);
   a.reward = out->reward;
   a.terminated = out->terminated;
   a.reward_f64 = out->reward_f64;
@@ -275,6 +281,32 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   DeviceGuard g(env->device);
   hipError_t st = launch_step(env->d, env->d_rows, env->d_dtab, d_actions, a, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(env, st, "bb_step");
+  return BB_OK;
+}
+
+int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions, const bb_rollout_out* out, void* stream) {
+  if (!env) return BB_ERR_ARG;
+  if (steps < 0) return fail(env, BB_ERR_ARG, "bb_rollout: steps must be >= 0");
+  if (!d_actions || !out || !out->reward || !out->terminated)
+    return fail(env, BB_ERR_ARG, "bb_rollout: actions, reward and terminated are required");
+  if (env->dbg) return fail(env, BB_ERR_STATE, "bb_rollout: not available in BB_DEBUG_MODE");
+  if (steps == 0) return BB_OK;
+  StepArgs a = base_args(env);
+  a.policy_seed = out->policy_seed;
+  a.env_offset = out->env_offset;
+  RollArgs r{};
+  r.steps = steps;
+  r.first_action = d_actions;
+  r.reward = out->reward;
+  r.terminated = out->terminated;
+  r.lines = out->lines;
+  r.actions = out->actions;
+  r.mask = out->mask;
+  r.next_action = out->next_action;
+  r.policy_step0 = out->policy_step0;
+  DeviceGuard g(env->device);
+  hipError_t st = launch_rollout(env->d, env->d_rows, env->d_dtab, a, r, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_rollout");
   return BB_OK;
 }
 

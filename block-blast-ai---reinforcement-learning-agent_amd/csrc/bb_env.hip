@@ -113,6 +113,55 @@ __device__ __forceinline__ uint64_t pack_pending(int attempt, int nblk, int line
          ((uint64_t)(uint32_t)gained << 32);
 }
 
+// Validity check and make_move of one lane's action (block_blast_env.py:237-245
+// -> engine.py:326-346 can_place_piece, 406-429 place / clear / score).  On a
+// legal move that used the last slot, returns true with s.drew set and the
+// used bits cleared: the caller draws the new hand (engine.py:432-437).
+__device__ __forceinline__ bool apply_move(const Tables& t, StepCtx& s, int act) {
+  s.drew = false;
+  s.nblk = 0;
+  s.lines = 0;
+  s.cm = 1;
+  s.gained = 0;
+  const int p = act >> 6;     // a // 64 for a >= 0
+  const int cell = act & 63;  // r*8 + c
+  uint32_t used = hand_used(s.hand);
+  bool valid = act >= 0 && act < 192 && !hand_over(s.hand) && !((used >> p) & 1u);
+  PieceRow pr{};
+  if (valid) {
+    pr = t.row[hand_id(s.hand, p)];
+    valid = ((pr.anchors >> cell) & 1ull) && ((pr.shape << cell) & s.B) == 0;
+  }
+  s.valid = valid;
+  if (!valid) return false;
+  s.nblk = (int)pr.ncells;
+  used |= 1u << p;
+  s.moves += 1;
+  s.blocks += s.nblk;
+  int rows, cols;
+  s.B = clear_full(s.B | (pr.shape << cell), rows, cols);
+  s.lines = rows + cols;
+  if (s.lines > 0) {
+    s.combo += 1;
+    s.max_combo = s.combo > s.max_combo ? s.combo : s.max_combo;
+    s.lines_tot += s.lines;
+    s.cm = s.lines < 4 ? s.lines : 4;
+    const int streak = s.combo + 1 < 8 ? s.combo + 1 : 8;  // post-increment combo (engine.py:261)
+    s.gained = s.nblk + (int64_t)(s.lines * 8 * 10) * s.cm * streak;  // blocks_in_lines = lines*8 (engine.py:427)
+  } else {
+    s.combo = 0;
+    s.gained = s.nblk;
+  }
+  s.score += s.gained;
+  if (used == 7u) {
+    s.drew = true;
+    s.hand &= ~(7u << 18);
+    return true;
+  }
+  s.hand = (s.hand & 0x3FFFFu) | (used << 18) | (s.hand & (1u << 22));
+  return false;
+}
+
 // ---------------------------------------------------------------------------
 // reset: engine.py:127-153 + block_blast_env.py:210-217
 // ---------------------------------------------------------------------------
@@ -154,6 +203,29 @@ __device__ __forceinline__ void store_reset(const EnvDev& e, int i, const Pcg& r
   e.mask[3 * i + 2] = m[2];
 }
 
+// _calculate_reward of a legal move (block_blast_env.py:158-193): fp64 in the
+// reference's exact operation order.  holes / center: the post-move values
+// that become _prev_holes / the filled-centre count.
+__device__ __forceinline__ double move_reward(const StepCtx& s, const StepArgs& a, bool over, int& holes,
+                                              int& center) {
+  double R = 0.0;
+  R = __dadd_rn(R, __dmul_rn((double)s.nblk, a.cfg.block_placed));
+  R = __dadd_rn(R, a.cfg.survival_bonus);
+  if (s.lines > 0) {
+    double lr = __dmul_rn((double)s.lines, a.cfg.line_clear_base);
+    lr = __dmul_rn(lr, (double)s.cm);
+    R = __dadd_rn(R, lr);
+    if (s.cm > 1) R = __dadd_rn(R, __dmul_rn((double)(s.cm - 1), a.cfg.combo_multiplier_bonus));
+  }
+  if (over) R = __dadd_rn(R, a.cfg.game_over_penalty);
+  holes = count_holes(s.B);
+  const int dh = holes - (int)(s.prev & 0xFFu);
+  if (dh > 0) R = __dadd_rn(R, __dmul_rn((double)dh, a.cfg.hole_penalty));
+  center = __popcll(s.B & kCenter);
+  if (center <= (int)(s.prev >> 8)) R = __dadd_rn(R, a.center_tenth);  // openness >= previous
+  return R;
+}
+
 // ---------------------------------------------------------------------------
 // finalize: game over, shaped reward, info, auto-reset, mask, policy, stores
 // ---------------------------------------------------------------------------
@@ -170,23 +242,7 @@ __device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepC
   if (s.valid) {
     const bool over = (m[0] | m[1] | m[2]) == 0ull;  // engine.py:440-441
     if (over) s.hand |= 1u << 21;
-    // _calculate_reward: block_blast_env.py:158-193, fp64 in this exact order
-    double R = 0.0;
-    R = __dadd_rn(R, __dmul_rn((double)s.nblk, a.cfg.block_placed));
-    R = __dadd_rn(R, a.cfg.survival_bonus);
-    if (s.lines > 0) {
-      double lr = __dmul_rn((double)s.lines, a.cfg.line_clear_base);
-      lr = __dmul_rn(lr, (double)s.cm);
-      R = __dadd_rn(R, lr);
-      if (s.cm > 1) R = __dadd_rn(R, __dmul_rn((double)(s.cm - 1), a.cfg.combo_multiplier_bonus));
-    }
-    if (over) R = __dadd_rn(R, a.cfg.game_over_penalty);
-    holes = count_holes(s.B);
-    const int dh = holes - (int)(s.prev & 0xFFu);
-    if (dh > 0) R = __dadd_rn(R, __dmul_rn((double)dh, a.cfg.hole_penalty));
-    center = __popcll(s.B & kCenter);
-    if (center <= (int)(s.prev >> 8)) R = __dadd_rn(R, a.center_tenth);  // openness >= previous
-    rew = R;
+    rew = move_reward(s, a, over, holes, center);
     term = over;
   } else if (a.info) {
     holes = count_holes(s.B);
@@ -320,53 +376,18 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
   const uint64_t T1 = prof ? __builtin_amdgcn_s_memtime() : 0;
   if (!live) return;
   s.rng.has = hand_has32(s.hand);
-  s.drew = false;
-  s.nblk = 0;
-  s.lines = 0;
-  s.cm = 1;
-  s.gained = 0;
 
-  // ---- validity: block_blast_env.py:237-245 -> engine.py:326-346 ----------
-  const int p = act >> 6;     // a // 64 for a >= 0
-  const int cell = act & 63;  // r*8 + c
-  uint32_t used = hand_used(s.hand);
-  bool valid = act >= 0 && act < 192 && !hand_over(s.hand) && !((used >> p) & 1u);
-  PieceRow pr{};
-  if (valid) {
-    pr = t.row[hand_id(s.hand, p)];
-    valid = ((pr.anchors >> cell) & 1ull) && ((pr.shape << cell) & s.B) == 0;
-  }
-  s.valid = valid;
+  // ---- validity + make_move: block_blast_env.py:237-245, engine.py:326-429
+  const bool draw = apply_move(t, s, act);
+  const bool valid = s.valid;
   const uint64_t T2 = prof ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t T3 = T2;
 
   if (valid) {
-    // ---- make_move: engine.py:406-429 ------------------------------------
-    s.nblk = (int)pr.ncells;
-    used |= 1u << p;
-    s.moves += 1;
-    s.blocks += s.nblk;
-    int rows, cols;
-    s.B = clear_full(s.B | (pr.shape << cell), rows, cols);
-    s.lines = rows + cols;
-    if (s.lines > 0) {
-      s.combo += 1;
-      s.max_combo = s.combo > s.max_combo ? s.combo : s.max_combo;
-      s.lines_tot += s.lines;
-      s.cm = s.lines < 4 ? s.lines : 4;
-      const int streak = s.combo + 1 < 8 ? s.combo + 1 : 8;  // post-increment combo (engine.py:261)
-      s.gained = s.nblk + (int64_t)(s.lines * 8 * 10) * s.cm * streak;  // blocks_in_lines = lines*8 (engine.py:427)
-    } else {
-      s.combo = 0;
-      s.gained = s.nblk;
-    }
-    s.score += s.gained;
     uint32_t ids = s.hand & 0x3FFFFu;
     if (prof) T3 = __builtin_amdgcn_s_memtime();
-    if (used == 7u) {
+    if (draw) {
       // ---- all three used -> new hand (engine.py:432-437) ---------------
-      used = 0;
-      s.drew = true;
       int attempt = 0;
       bool done;
       if (a.dbg & 1) {  // diagnostics only: first draw, no solvability test (NOT reference semantics)
@@ -411,8 +432,6 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
         }
         return;
       }
-    } else {
-      s.hand = ids | (used << 18) | (s.hand & (1u << 22));
     }
   }
   const uint64_t T4 = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -506,6 +525,149 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
     s.hand = my_ids | ((uint32_t)s.rng.has << 22);
     finalize(t, e, s, a);
     e.pend[mine] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// rollout: T steps of every env in one launch under the fused random policy
+// (BASELINE config 2).  State stays in VGPRs for the whole rollout; a wave
+// owns kRollEnvs envs (one per lane) and runs their hand searches itself,
+// one parked env at a time with all 64 lanes (gen_hand_wave), so a hard
+// search delays only its own wave and the per-step tail of the two-kernel
+// bb_step averages out over the T steps.  Output for output identical to T
+// bb_step calls chained through next_action (wrappers.py:128-137
+// sample_valid_actions -> step, with the Philox policy in place of
+// np.random.choice).
+// ---------------------------------------------------------------------------
+#ifndef BB_ROLL_ENVS
+#define BB_ROLL_ENVS 64
+#endif
+constexpr int kRollEnvs = BB_ROLL_ENVS;  // envs per wave (64, or 32 for two waves per SIMD at 65,536 envs)
+#ifndef BB_ROLL_BLOCK
+#define BB_ROLL_BLOCK 64
+#endif
+constexpr int kRollBlock = BB_ROLL_BLOCK;
+
+__global__ void __launch_bounds__(kRollBlock) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
+                                                             StepArgs a, RollArgs r) {
+  __shared__ Tables t;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * kRollBlock + threadIdx.x) >> 6;
+  const int i = wave * kRollEnvs + lane;
+  const bool live = lane < kRollEnvs && i < e.n;
+  StepCtx s;
+  int act = 0;
+  uint64_t m[3] = {0ull, 0ull, 0ull};
+  if (live) {
+    s.i = i;
+    act = r.first_action[i];
+    s.B = e.board[i];
+    s.hand = e.hand[i];
+    s.score = e.score[i];
+    s.combo = e.combo[i];
+    s.max_combo = e.max_combo[i];
+    s.moves = e.moves[i];
+    s.lines_tot = e.lines[i];
+    s.blocks = e.blocks[i];
+    s.prev = e.prev[i];
+    s.rng.hi = e.rng_hi[i];
+    s.rng.lo = e.rng_lo[i];
+    s.rng.buf = e.rng_buf[i];
+    s.rng.inc_hi = e.inc_hi[i];
+    s.rng.inc_lo = e.inc_lo[i];
+    s.seed_hi = e.seed_hi[i];
+    s.seed_lo = e.seed_lo[i];
+    s.has_seed = e.has_seed[i] != 0;
+    m[0] = e.mask[3 * i + 0];
+    m[1] = e.mask[3 * i + 1];
+    m[2] = e.mask[3 * i + 2];
+  }
+  stage_tables(t, g_rows, g_d);
+  if (__ballot(live) == 0ull) return;  // wave-uniform
+  if (live) s.rng.has = hand_has32(s.hand);
+  const size_t N = (size_t)e.n;
+#pragma unroll 1
+  for (int step = 0; step < r.steps; ++step) {
+    bool park = false;
+    if (live) {
+      if (apply_move(t, s, act)) {
+        uint32_t ids = 0;
+        park = !quick_hand(s.B, s.rng, ids, t.row, t.d, a.lane_quick);  // rolls back on failure
+        s.hand = ids | ((uint32_t)s.rng.has << 22);
+      }
+    }
+    // hand searches the in-lane test left open: the whole wave, one env at a time
+    uint64_t parked = __ballot(park);
+    while (parked) {
+      const int k = __ffsll((unsigned long long)parked) - 1;
+      parked &= parked - 1;
+      Pcg w;
+      w.hi = __shfl(s.rng.hi, k);
+      w.lo = __shfl(s.rng.lo, k);
+      w.inc_hi = __shfl(s.rng.inc_hi, k);
+      w.inc_lo = __shfl(s.rng.inc_lo, k);
+      w.buf = __shfl(s.rng.buf, k);
+      w.has = __shfl((int)s.rng.has, k) != 0;
+      const uint64_t wB = __shfl(s.B, k);
+      uint32_t ids = 0;
+      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next);
+      if (lane == k) {
+        s.rng = w;
+        s.hand = ids | ((uint32_t)w.has << 22);
+      }
+    }
+    if (live) {
+      masks_of(t, s.B, s.hand, m);
+      double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
+      bool term = false;
+      if (s.valid) {
+        const bool over = (m[0] | m[1] | m[2]) == 0ull;  // engine.py:440-441
+        if (over) s.hand |= 1u << 21;
+        int holes, center;
+        rew = move_reward(s, a, over, holes, center);
+        s.prev = (uint32_t)(holes | (center << 8));
+        term = over;
+      }
+      const size_t o = (size_t)step * N + (size_t)i;
+      r.reward[o] = (float)rew;
+      r.terminated[o] = term ? 1 : 0;
+      if (r.lines) r.lines[o] = (uint8_t)s.lines;
+      if (r.actions) r.actions[o] = act;
+      if (term && a.autoreset) {  // wrappers.py:97-102
+        reset_lane(t, s.has_seed, s.seed_hi, s.seed_lo, s.rng, s.B, s.hand, m);
+        s.score = 0;
+        s.combo = 0;
+        s.max_combo = 0;
+        s.moves = 0;
+        s.lines_tot = 0;
+        s.blocks = 0;
+        s.prev = 0;
+      }
+      if (r.mask) {
+        r.mask[3 * o + 0] = m[0];
+        r.mask[3 * o + 1] = m[1];
+        r.mask[3 * o + 2] = m[2];
+      }
+      act = random_policy(m[0], m[1], m[2], a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + step + 1);
+    }
+  }
+  if (live) {
+    e.board[i] = s.B;
+    e.hand[i] = s.hand;
+    e.rng_hi[i] = s.rng.hi;
+    e.rng_lo[i] = s.rng.lo;
+    e.rng_buf[i] = s.rng.buf;
+    e.score[i] = s.score;
+    e.combo[i] = s.combo;
+    e.max_combo[i] = s.max_combo;
+    e.moves[i] = s.moves;
+    e.lines[i] = s.lines_tot;
+    e.blocks[i] = s.blocks;
+    e.prev[i] = (uint16_t)s.prev;
+    e.mask[3 * i + 0] = m[0];
+    e.mask[3 * i + 1] = m[1];
+    e.mask[3 * i + 2] = m[2];
+    if (r.next_action) r.next_action[i] = act;
   }
 }
 
@@ -621,6 +783,14 @@ hipError_t launch_step(const EnvDev& e, const PieceRow* rows, const uint8_t* d, 
   const int envs_per_block = kEscBlock / 64 * kEscGroup;
   hipLaunchKernelGGL(escalate_kernel, dim3((e.n + envs_per_block - 1) / envs_per_block), dim3(kEscBlock), 0, s, e,
                      rows, d, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const StepArgs& a,
+                          const RollArgs& r, hipStream_t s) {
+  const int64_t waves = ((int64_t)e.n + kRollEnvs - 1) / kRollEnvs;
+  const int64_t blocks = (waves * 64 + kRollBlock - 1) / kRollBlock;
+  hipLaunchKernelGGL(rollout_kernel, dim3((unsigned)blocks), dim3(kRollBlock), 0, s, e, rows, d, a, r);
   return hipGetLastError();
 }
 

@@ -60,9 +60,24 @@ struct StepArgs {
   uint64_t env_offset;
 };
 
+// bb_rollout: T fused steps (see rollout_kernel).  Per-step outputs are [T][N].
+struct RollArgs {
+  int steps;
+  const int32_t* first_action;  // [N] action of step 0
+  float* reward;                // [T][N]
+  uint8_t* terminated;          // [T][N]
+  uint8_t* lines;               // [T][N] optional
+  int32_t* actions;             // [T][N] optional: action applied at step t
+  uint64_t* mask;               // [T][N][3] optional: post-step mask bits
+  int32_t* next_action;         // [N] optional: policy action after the last step
+  uint64_t policy_step0;        // step t's next action uses policy_step0 + t + 1
+};
+
 hipError_t launch_reset(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const uint8_t* sel, hipStream_t s);
 hipError_t launch_step(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const int32_t* actions,
                        const StepArgs& a, hipStream_t s);
+hipError_t launch_rollout(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const StepArgs& a,
+                          const RollArgs& r, hipStream_t s);
 hipError_t launch_expand(const uint64_t* board, const uint32_t* hand, const uint64_t* mbits, const int64_t* index,
                          const PieceRow* rows, int n, float* x, float* mf, int8_t* mi, hipStream_t s);
 hipError_t launch_refresh_mask(const EnvDev& e, const PieceRow* rows, hipStream_t s);

@@ -163,6 +163,40 @@ class DeviceEnvBatch:
         L.check(self.lib.bb_step(self.handle, _ptr(actions), C.byref(o), _stream(self.device)), "bb_step",
                 self.handle)
 
+    def rollout(
+        self,
+        steps: int,
+        actions: torch.Tensor,
+        reward: torch.Tensor,
+        terminated: torch.Tensor,
+        lines: Optional[torch.Tensor] = None,
+        actions_out: Optional[torch.Tensor] = None,
+        mask_out: Optional[torch.Tensor] = None,
+        next_action: Optional[torch.Tensor] = None,
+        policy_seed: int = 0xB10C,
+        policy_step0: int = 0,
+    ) -> None:
+        """``steps`` fused steps under the synthetic random policy (bb_rollout).
+        actions: int32 [N], the action of the first step; reward f32 / terminated
+        u8 / lines u8 / actions_out i32 are [steps, N], mask_out i64 [steps, N, 3].
+        Equals ``steps`` chained ``step(..., next_action=, policy_step=policy_step0+t+1)``."""
+        n = self.num_envs
+        assert actions.dtype == torch.int32 and actions.is_cuda and actions.numel() == n
+        assert reward.dtype == torch.float32 and reward.numel() >= steps * n
+        assert terminated.dtype == torch.uint8 and terminated.numel() >= steps * n
+        for t, dt, per in ((lines, torch.uint8, 1), (actions_out, torch.int32, 1), (mask_out, torch.int64, 3),
+                           (next_action, torch.int32, 0)):
+            if t is not None:
+                assert t.dtype == dt and t.is_cuda and t.numel() >= (steps * n * per if per else n)
+        o = L.RolloutOut(reward=reward.data_ptr(), terminated=terminated.data_ptr(),
+                         lines=lines.data_ptr() if lines is not None else None,
+                         actions=actions_out.data_ptr() if actions_out is not None else None,
+                         mask=mask_out.data_ptr() if mask_out is not None else None,
+                         next_action=next_action.data_ptr() if next_action is not None else None,
+                         policy_seed=policy_seed, policy_step0=policy_step0, env_offset=self.env_offset)
+        L.check(self.lib.bb_rollout(self.handle, int(steps), _ptr(actions), C.byref(o), _stream(self.device)),
+                "bb_rollout", self.handle)
+
     def obs(self, x=None, mask_i8=None, mask_f32=None, mask_bits=None) -> None:
         L.check(
             self.lib.bb_obs(self.handle, _ptr(x), _ptr(mask_i8), _ptr(mask_f32), _ptr(mask_bits),

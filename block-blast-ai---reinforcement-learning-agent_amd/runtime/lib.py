@@ -73,6 +73,20 @@ class StepOut(C.Structure):
     ]
 
 
+class RolloutOut(C.Structure):
+    _fields_ = [
+        ("reward", C.c_void_p),
+        ("terminated", C.c_void_p),
+        ("lines", C.c_void_p),
+        ("actions", C.c_void_p),
+        ("mask", C.c_void_p),
+        ("next_action", C.c_void_p),
+        ("policy_seed", C.c_uint64),
+        ("policy_step0", C.c_uint64),
+        ("env_offset", C.c_uint64),
+    ]
+
+
 class StateView(C.Structure):
     _fields_ = [
         ("board", C.c_void_p),
@@ -105,6 +119,7 @@ SIGNATURES = {
     "bb_seed": (C.c_int, [_P, _P, _P, _P]),
     "bb_reset": (C.c_int, [_P, _P, _P]),
     "bb_step": (C.c_int, [_P, _P, C.POINTER(StepOut), _P]),
+    "bb_rollout": (C.c_int, [_P, _I32, _P, C.POINTER(RolloutOut), _P]),
     "bb_obs": (C.c_int, [_P, _P, _P, _P, _P, _P]),
     "bb_device_ptrs": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P)]),
     "bb_snapshot": (C.c_int, [_P, _P, _P, _P, _P]),

@@ -152,6 +152,30 @@ int bb_reset(bb_env* env, const uint8_t* d_env_mask, void* stream);
 int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out,
             void* stream);
 
+/* T steps of every env in ONE launch under the fused synthetic random policy
+ * (BASELINE config 2; the reference's rollout loop of wrappers.py:128-137
+ * sample_valid_actions -> wrappers.py:75-116 step, with the Philox policy of
+ * bb_step_out.next_action in place of np.random.choice).  Output for output
+ * and in the final state it equals T chained bb_step calls: call t takes
+ * d_actions (t = 0) or call t-1's next_action, with policy_step =
+ * policy_step0 + t + 1.  Per-step outputs are [T][N] (t-major); the env
+ * state stays in registers between steps, so nothing but these outputs
+ * touches HBM inside the rollout. */
+typedef struct bb_rollout_out {
+  float* reward;          /* [T][N] f32, required                             */
+  uint8_t* terminated;    /* [T][N] 0/1, required                             */
+  uint8_t* lines;         /* [T][N] optional: lines cleared by each move      */
+  int32_t* actions;       /* [T][N] optional: the action applied at step t    */
+  uint64_t* mask;         /* [T][N][3] optional: post-step (post-reset) masks */
+  int32_t* next_action;   /* [N] optional: policy action after the last step  */
+  uint64_t policy_seed;
+  uint64_t policy_step0;
+  uint64_t env_offset;    /* global index of env 0 (multi-GPU shards)         */
+} bb_rollout_out;
+
+int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions,
+               const bb_rollout_out* out, void* stream);
+
 /* Observation expansion (engine.py:478-507, block_blast_env.py:134-146,
  * wrappers.py:118-126).  Any output may be NULL:
  *   d_x      [N][4][8][8] f32: plane 0 board, planes 1-3 unused piece shapes
