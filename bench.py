@@ -4,19 +4,23 @@
 Default workload (BASELINE config 2, one GPU): 65,536 envs per GPU, env i
 seeded 42 + global index, HIP bitboard step + action mask + in-kernel
 auto-reset, actions from the synthetic random policy (Philox, fused into the
-step kernel).  One "step" = one bb_step launch over the whole batch.
+kernel).  One "step" = one env-step of the whole batch.  The default
+`--mode rollout` runs T = 128 steps (the reference's PPO horizon) per
+bb_rollout launch with the env state held in registers; `--mode step` runs
+one bb_step launch (step + escalate kernels) per step, the drop-in path under
+VectorizedBlockBlastEnv.step.  Both produce identical trajectories
+(tests/test_gpu_rollout.py).
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W [--mode rollout|step]
     (N > 1: launched by torch.distributed.run, one rank per GPU; envs are
      independent shards, no collective on the data path -> weak scaling)
 
-Prints ONE JSON line on rank 0.  `roofline` prices the step kernel against
-HBM with the algorithmic bytes of SURVEY.md 8(d) (194 B per env-step) over its
-average launch duration measured here with HIP events on the launch stream
-(one bb_step = bb::step_kernel + bb::escalate_kernel, back to back on that
-stream; the rocprofv3 kernel-trace sum of the two agrees, profiles/);
-`cpu_baseline` times the CPU port of the reference's 64-env vectorised path
-(oracle/bb_game.py, one core) on a bounded sample.
+Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel
+against HBM with the algorithmic bytes of SURVEY.md 8(d) (194 B per env-step)
+x the env-steps of one launch, over its average launch duration measured here
+with HIP events on the launch stream (the rocprofv3 kernel-trace average
+agrees, profiles/); `cpu_baseline` times the CPU port of the reference's
+64-env vectorised path (oracle/bb_game.py, one core) on a bounded sample.
 """
 from __future__ import annotations
 
@@ -69,15 +73,16 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
     }
 
 
-def load_traffic(n_envs: int):
-    """HBM bytes per step-kernel launch from a committed rocprofv3 PMC run
-    (profiles/pmc_step_kernel.json, written by tools/pmc_traffic.py from two
-    separate --pmc passes, FETCH_SIZE doubled per the gfx950 note), or None."""
-    p = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
+def load_traffic(n_envs: int, mode: str, steps_per_launch: int):
+    """HBM bytes per launch from a committed rocprofv3 PMC run
+    (profiles/pmc_step_kernel.json or pmc_rollout_kernel.json, written by
+    tools/pmc_traffic.py from two separate --pmc passes, FETCH_SIZE doubled
+    per the gfx950 note), or None when it was taken on another shape."""
+    p = os.path.join(REPO, "profiles", f"pmc_{mode}_kernel.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if int(d.get("n_envs", -1)) == n_envs:
+        if int(d.get("n_envs", -1)) == n_envs and int(d.get("steps_per_launch", 1)) == steps_per_launch:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -92,9 +97,10 @@ def main() -> None:
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--mode", choices=("step", "rollout"), default="step",
-                    help="step: one bb_step launch per env-step; rollout: bb_rollout, T fused steps per launch")
-    ap.add_argument("--rollout-len", type=int, default=50, help="T, env-steps per bb_rollout launch")
+    ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
+                    help="rollout: bb_rollout, T fused env-steps per launch (default); step: one bb_step per env-step")
+    ap.add_argument("--rollout-len", type=int, default=128,
+                    help="T, env-steps per bb_rollout launch (default 128 = the reference's PPO horizon n_steps)")
     args = ap.parse_args()
 
     import torch
@@ -173,7 +179,9 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # average bb_step (both kernels + their launch gap)
+    # average launch: bb_step (both kernels + their gap) or one full T-step bb_rollout
+    per_launch = 1 if args.mode == "step" else T
+    kern_ms = ev0.elapsed_time(ev1) / args.steps * per_launch
     if world > 1:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device="cpu" if share else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -186,9 +194,9 @@ def main() -> None:
     total_env_steps = n * world * args.steps
     value = total_env_steps / el
     if rank == 0:
-        algo_bytes = ALGO_BYTES_PER_ENV_STEP * n
+        algo_bytes = ALGO_BYTES_PER_ENV_STEP * n * per_launch
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(n)
+        traffic = load_traffic(n, args.mode, per_launch)
         out = {
             "metric": "env-steps/sec (whole node) at 64k parallel envs, 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -205,6 +213,7 @@ def main() -> None:
             "config": {
                 "workload": "BASELINE config 2: 65,536 envs per MI355X, HIP bitboard step + action mask + "
                             "auto-reset, random policy (env throughput)",
+                "mode": args.mode if args.mode == "step" else f"rollout T={T}",
                 "envs_per_gpu": n,
                 "global_envs": n * world,
                 "parallelism": f"env shards x{world} (no data-path collective)",
@@ -217,7 +226,8 @@ def main() -> None:
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "kernel": ("bb_step = bb::step_kernel + bb::escalate_kernel" if args.mode == "step" else
-                           f"bb_rollout = bb::rollout_kernel, {T} env-steps per launch (time per env-step)"),
+                           f"bb_rollout = bb::rollout_kernel, {T} env-steps of every env per launch"),
+                "env_steps_per_launch": n * per_launch,
                 "kernel_avg_ms": round(kern_ms, 5),
                 "algo_bytes_per_launch": algo_bytes,
             },

@@ -197,8 +197,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
     delete e;
     return fail(nullptr, BB_ERR_HIP, m);
   }
-  if (e->dbg & 14) {
-    if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~14;
+  if (e->dbg & 30) {
+    if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~30;
     else (void)hipMemset(e->dbg_out, 0, n * 32);
   }
   *out = e;
@@ -289,7 +289,7 @@ int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions, const bb_ro
   if (steps < 0) return fail(env, BB_ERR_ARG, "bb_rollout: steps must be >= 0");
   if (!d_actions || !out || !out->reward || !out->terminated)
     return fail(env, BB_ERR_ARG, "bb_rollout: actions, reward and terminated are required");
-  if (env->dbg) return fail(env, BB_ERR_STATE, "bb_rollout: not available in BB_DEBUG_MODE");
+  if (env->dbg & ~16) return fail(env, BB_ERR_STATE, "bb_rollout: only BB_DEBUG_MODE=16 (rollout phase counters)");
   if (steps == 0) return BB_OK;
   StepArgs a = base_args(env);
   a.policy_seed = out->policy_seed;

@@ -540,15 +540,21 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
 // np.random.choice).
 // ---------------------------------------------------------------------------
 #ifndef BB_ROLL_ENVS
-#define BB_ROLL_ENVS 64
+#define BB_ROLL_ENVS 32
 #endif
-constexpr int kRollEnvs = BB_ROLL_ENVS;  // envs per wave (64, or 32 for two waves per SIMD at 65,536 envs)
+// Envs per wave.  Fewer envs than lanes means more waves per SIMD (2 at
+// 65,536 envs with 32), which hides the LDS / dependent-ALU latency of the
+// searches; lanes >= kRollEnvs join the wave-cooperative searches only.
+constexpr int kRollEnvs = BB_ROLL_ENVS;
 #ifndef BB_ROLL_BLOCK
 #define BB_ROLL_BLOCK 64
 #endif
 constexpr int kRollBlock = BB_ROLL_BLOCK;
+#ifndef BB_ROLL_MINW
+#define BB_ROLL_MINW 1
+#endif
 
-__global__ void __launch_bounds__(kRollBlock) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
+__global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a, RollArgs r) {
   __shared__ Tables t;
   const int lane = threadIdx.x & 63;
@@ -586,18 +592,39 @@ __global__ void __launch_bounds__(kRollBlock) rollout_kernel(EnvDev e, const Pie
   if (__ballot(live) == 0ull) return;  // wave-uniform
   if (live) s.rng.has = hand_has32(s.hand);
   const size_t N = (size_t)e.n;
+#if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3  // timing diagnostics: per-wave phase cycles (reference semantics)
+  uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // move+quick, searches, finalize, #searches, attempts, passes, slow passes
+  uint32_t st[8];
+#define BB_DIAG_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
+#else
+#define BB_DIAG_T(x)
+#endif
 #pragma unroll 1
   for (int step = 0; step < r.steps; ++step) {
+    BB_DIAG_T(c0);
     bool park = false;
     if (live) {
       if (apply_move(t, s, act)) {
         uint32_t ids = 0;
+#if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 2  // timing diagnostics only: first draw, no test (NOT reference)
+        ids = draw_piece(s.rng);
+        ids |= draw_piece(s.rng) << 6;
+        ids |= draw_piece(s.rng) << 12;
+#elif defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 1  // timing diagnostics only: no wave search (NOT reference)
+        if (!quick_hand(s.B, s.rng, ids, t.row, t.d, a.lane_quick)) {
+          ids = draw_piece(s.rng);
+          ids |= draw_piece(s.rng) << 6;
+          ids |= draw_piece(s.rng) << 12;
+        }
+#else
         park = !quick_hand(s.B, s.rng, ids, t.row, t.d, a.lane_quick);  // rolls back on failure
+#endif
         s.hand = ids | ((uint32_t)s.rng.has << 22);
       }
     }
     // hand searches the in-lane test left open: the whole wave, one env at a time
     uint64_t parked = __ballot(park);
+    BB_DIAG_T(c1);
     while (parked) {
       const int k = __ffsll((unsigned long long)parked) - 1;
       parked &= parked - 1;
@@ -610,12 +637,23 @@ __global__ void __launch_bounds__(kRollBlock) rollout_kernel(EnvDev e, const Pie
       w.has = __shfl((int)s.rng.has, k) != 0;
       const uint64_t wB = __shfl(s.B, k);
       uint32_t ids = 0;
+#if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
+      for (int q = 0; q < 8; ++q) st[q] = 0;
+      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, st);
+      dg[3] += 1;
+      dg[4] += st[0];
+      dg[5] += st[1] | ((uint64_t)st[2] << 32);
+      dg[6] += st[4];
+      dg[7] += st[5] | ((uint64_t)st[6] << 32);
+#else
       gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next);
+#endif
       if (lane == k) {
         s.rng = w;
         s.hand = ids | ((uint32_t)w.has << 22);
       }
     }
+    BB_DIAG_T(c2);
     if (live) {
       masks_of(t, s.B, s.hand, m);
       double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
@@ -650,7 +688,17 @@ __global__ void __launch_bounds__(kRollBlock) rollout_kernel(EnvDev e, const Pie
       }
       act = random_policy(m[0], m[1], m[2], a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + step + 1);
     }
+#if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
+    BB_DIAG_T(c3);
+    dg[0] += c1 - c0;
+    dg[1] += c2 - c1;
+    dg[2] += c3 - c2;
+#endif
   }
+#if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
+  if (lane == 0 && a.dbg_out)
+    for (int q = 0; q < 8; ++q) a.dbg_out[8 * wave + q] = dg[q];
+#endif
   if (live) {
     e.board[i] = s.B;
     e.hand[i] = s.hand;
