@@ -449,6 +449,7 @@ __global__ void __launch_bounds__(kStepBlock) step_kernel(EnvDev e, const PieceR
 __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a) {
   __shared__ Tables t;
+  __shared__ uint32_t scratch[kEscBlock];  // 64 words per wave (slow_phase_wave)
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * kEscBlock + threadIdx.x) >> 6;
   const int base = wave * kEscGroup;
@@ -506,8 +507,9 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
     const int watt = __shfl((int)(pr & 0xFFu), k);
     uint32_t ids = 0;
     const uint64_t c0 = (a.dbg & 2) ? __builtin_amdgcn_s_memtime() : 0;
-    uint32_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    gen_hand_wave(wB, w, ids, watt, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, (a.dbg & 2) ? st : nullptr);
+    uint32_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    gen_hand_wave(wB, w, ids, watt, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next,
+                  scratch + (threadIdx.x & ~63), (a.dbg & 2) ? st : nullptr);
     if ((a.dbg & 2) && lane == 0) {
       a.dbg_out[4 * (base + k) + 2] = __builtin_amdgcn_s_memtime() - c0;
       a.dbg_out[4 * (base + k) + 1] = (uint64_t)st[0] | ((uint64_t)st[1] << 16) | ((uint64_t)st[2] << 32) |
@@ -557,6 +559,8 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a, RollArgs r) {
   __shared__ Tables t;
+  __shared__ uint32_t scratch[kRollBlock];  // 64 words per wave (slow_phase_wave)
+  uint32_t* lds = scratch + (threadIdx.x & ~63);
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * kRollBlock + threadIdx.x) >> 6;
   const int i = wave * kRollEnvs + lane;
@@ -593,8 +597,10 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   if (live) s.rng.has = hand_has32(s.hand);
   const size_t N = (size_t)e.n;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3  // timing diagnostics: per-wave phase cycles (reference semantics)
-  uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // move+quick, searches, finalize, #searches, attempts, passes, slow passes
-  uint32_t st[8];
+  // move+quick, searches, finalize, #searches, attempts | 1-attempt searches << 32, passes | slow passes << 32,
+  // quick cycles | slots << 32, disjoint | line cycles << 32
+  uint64_t dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t st[12];
 #define BB_DIAG_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
 #else
 #define BB_DIAG_T(x)
@@ -638,15 +644,16 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       const uint64_t wB = __shfl(s.B, k);
       uint32_t ids = 0;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
-      for (int q = 0; q < 8; ++q) st[q] = 0;
-      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, st);
-      dg[3] += 1;
-      dg[4] += st[0];
+      for (int q = 0; q < 12; ++q) st[q] = 0;
+      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, lds, st);
+      dg[3] += 1 | ((uint64_t)st[9] << 32);
+      dg[4] += st[0] | ((uint64_t)(st[0] == 1 ? 1u : 0u) << 32);
       dg[5] += st[1] | ((uint64_t)st[2] << 32);
-      dg[6] += st[4];
+      dg[6] += st[4] | ((uint64_t)st[8] << 32);
       dg[7] += st[5] | ((uint64_t)st[6] << 32);
+      dg[8] += (st[0] == 1 && st[10] == 0) ? 1u : 0u;
 #else
-      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next);
+      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, lds);
 #endif
       if (lane == k) {
         s.rng = w;
@@ -697,7 +704,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   }
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
   if (lane == 0 && a.dbg_out)
-    for (int q = 0; q < 8; ++q) a.dbg_out[8 * wave + q] = dg[q];
+    for (int q = 0; q < 9; ++q) a.dbg_out[9 * wave + q] = dg[q];
 #endif
   if (live) {
     e.board[i] = s.B;

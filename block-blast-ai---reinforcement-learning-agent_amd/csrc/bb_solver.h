@@ -25,6 +25,10 @@
 #pragma once
 #include "bb_device.h"
 
+#ifndef BB_SLOW_FLAT
+#define BB_SLOW_FLAT 1  // flattened exact level 2 (slow_phase_wave); 0: per-lane disjoint scan + line phase
+#endif
+
 namespace bb {
 
 constexpr int kUnlimited = 1 << 30;
@@ -363,6 +367,92 @@ __device__ __forceinline__ bool line_phase_wave(uint64_t B1, uint32_t bi, uint32
 
 
 // ---------------------------------------------------------------------------
+// Wave64 cross-lane helpers on DPP (gfx9 row_shr / row_bcast): VALU-only, no
+// LDS round trip per step, unlike __shfl_up (ds_bpermute).
+// ---------------------------------------------------------------------------
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_zero(uint32_t x) {  // lanes out of range / in masked rows read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);
+}
+// Inclusive prefix sum over the 64 lanes.
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+  x += dpp_zero<0x111, 0xF>(x);  // row_shr:1
+  x += dpp_zero<0x112, 0xF>(x);  // row_shr:2
+  x += dpp_zero<0x114, 0xF>(x);  // row_shr:4
+  x += dpp_zero<0x118, 0xF>(x);  // row_shr:8
+  x += dpp_zero<0x142, 0xA>(x);  // row_bcast:15 into rows 1, 3
+  x += dpp_zero<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3
+  return x;
+}
+// Inclusive prefix max over the 64 lanes (values >= 0).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  x = max(x, dpp_zero<0x111, 0xF>(x));
+  x = max(x, dpp_zero<0x112, 0xF>(x));
+  x = max(x, dpp_zero<0x114, 0xF>(x));
+  x = max(x, dpp_zero<0x118, 0xF>(x));
+  x = max(x, dpp_zero<0x142, 0xA>(x));
+  x = max(x, dpp_zero<0x143, 0xC>(x));
+  return x;
+}
+// Order this wave's LDS accesses across lanes (one wave's DS instructions
+// execute in order; this only stops the compiler from moving them).
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Exact level 2 of the undecided slots, flattened over the wave: the
+// reference DFS's own leaf tests (engine.py:196-224 _can_place_remaining),
+// one per lane -- for every undecided slot, every anchor q of b (then c must
+// fit on clear(B1 | b@q)) and every anchor r of c (then b must fit on
+// clear(B1 | c@r)).  The tasks of all slots are dealt out 64 at a time; a
+// task's owner slot is found by scattering each slot's first task index to
+// LDS and taking a prefix max (DPP).  Returns this lane's slot verdict.
+// lds: 64 words of wave-private LDS scratch.  All lanes call it.
+__device__ __forceinline__ bool slow_phase_wave(bool need, uint64_t B1, uint32_t bi, uint32_t ci, uint64_t A2,
+                                                uint64_t A3, const PieceRow* tbl, int lane, uint32_t* lds) {
+  const uint32_t n2 = need ? (uint32_t)__popcll(A2) : 0u;
+  const uint32_t cnt = n2 + (need ? (uint32_t)__popcll(A3) : 0u);
+  const uint32_t incl = wave_incl_add(cnt);
+  const uint32_t off = incl - cnt;
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  uint64_t won_mask = 0ull;  // bit o: slot o has a successful leaf
+#pragma unroll 1
+  for (uint32_t base = 0; base < total; base += 64u) {
+    // owner of task base+lane: the last slot whose first task is <= it
+    wave_lds_fence();
+    lds[lane] = 0u;
+    wave_lds_fence();
+    if (cnt && off < base + 64u && incl > base) atomicMax(&lds[off > base ? off - base : 0u], (uint32_t)lane);
+    wave_lds_fence();
+    const int o = (int)wave_incl_max(lds[lane]);
+    const uint32_t t = base + (uint32_t)lane;
+    const uint64_t oB = __shfl(B1, o);
+    const uint64_t oA2 = __shfl(A2, o), oA3 = __shfl(A3, o);
+    const uint32_t oid = __shfl(bi | (ci << 8), o);
+    const uint32_t k = t - __shfl(off, o);
+    const uint32_t on2 = __shfl(n2, o);
+    bool hit = false;
+    if (t < total) {
+      const bool bfirst = k < on2;
+      const PieceRow& first = tbl[bfirst ? (oid & 0xFFu) : (oid >> 8)];
+      const PieceRow& second = tbl[bfirst ? (oid >> 8) : (oid & 0xFFu)];
+      const int pos = select_bit(bfirst ? oA2 : oA3, bfirst ? k : k - on2);
+      hit = anchors_of(second, clear_full(oB | (first.shape << pos))) != 0ull;
+    }
+    // owners with a hit: a wave-uniform mask (hits are rare; one readlane each)
+    uint64_t hits = __ballot(hit);
+    while (hits) {
+      const int l = __ffsll((unsigned long long)hits) - 1;
+      hits &= hits - 1;
+      won_mask |= 1ull << __builtin_amdgcn_readlane(o, l);
+    }
+  }
+  return (won_mask >> lane) & 1ull;
+}
+
+// ---------------------------------------------------------------------------
 // Wave-cooperative _generate_new_pieces (engine.py:155-172) for one env: all
 // 64 lanes call it with identical arguments; on return ids/rng are the final
 // hand and stream state, identical in every lane.
@@ -448,8 +538,8 @@ __device__ __forceinline__ bool draw_attempt_jump(const Pcg& s0, const JumpRow* 
 
 __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& ids, int attempt,
                                               const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
-                                              int lane, int pack_first, int pack_next,
-                                              uint32_t* stats = nullptr) {
+                                              int lane, int pack_first, int pack_next, uint32_t* lds,
+                                              uint32_t* stats = nullptr) {  // diagnostics: [12] counters
   const int attempt0 = attempt;
   // anchors of every piece on B: lane x holds piece x
   const uint64_t acache = lane < kPieces ? anchors_of(tbl[lane], B) : 0ull;
@@ -477,12 +567,7 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
     const uint64_t eA1 = __shfl(acache, (int)hand_id(e_ids, 1));
     const uint64_t eA2 = __shfl(acache, (int)hand_id(e_ids, 2));
     const uint32_t S = lane < nb_draw ? (uint32_t)(__popcll(eA0) + __popcll(eA1) + __popcll(eA2)) : 0u;
-    uint32_t incl = S;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(incl, o);
-      if (lane >= o) incl += u;
-    }
+    const uint32_t incl = wave_incl_add(S);
     const int e_off = (int)(incl - S);
     // attempts packed into this pass: the leading ones whose tasks fit 64
     int nb = __popcll(__ballot(lane < nb_draw && incl <= 64u));
@@ -541,16 +626,24 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
         stats[2] += needs ? 1u : 0u;
         const uint32_t sl = (uint32_t)(total - base < 64 ? total - base : 64);
         stats[3] = stats[3] > sl ? stats[3] : sl;
+        stats[8] += sl;
+        stats[9] += (uint32_t)__popcll(needs);
       }
       const uint64_t tq1 = stats ? __builtin_amdgcn_s_memtime() : 0;
       if (stats) stats[4] += (uint32_t)(tq1 - tq0);
       if (needs) {
+#if BB_SLOW_FLAT
+        const uint64_t tq2 = stats ? __builtin_amdgcn_s_memtime() : 0;
+        ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds);
+        uint64_t C2 = 0ull, C3 = 0ull;
+#else
         uint64_t C2 = 0ull, C3 = 0ull;
         if (need) {
           ok = pair_disjoint(B1, tbl[bi], tbl[ci], A2, A3, C2, C3) == 1;
         }
         const uint64_t tq2 = stats ? __builtin_amdgcn_s_memtime() : 0;
         if (__ballot((C2 | C3) != 0ull)) ok |= line_phase_wave(B1, bi, ci, C2, C3, tbl, lane);
+#endif
         if (stats) {
           const uint64_t tq3 = __builtin_amdgcn_s_memtime();
           stats[5] += (uint32_t)(tq2 - tq1);
@@ -569,7 +662,10 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
         rng.lo = __shfl(e_after.lo, jw);
         rng.buf = __shfl(e_after.buf, jw);
         rng.has = __shfl((int)e_after.has, jw) != 0;
-        if (stats) stats[0] = (uint32_t)(attempt + jw + 1 - attempt0);
+        if (stats) {
+          stats[0] = (uint32_t)(attempt + jw + 1 - attempt0);
+          stats[10] = needs ? 1u : 0u;  // decided by a pass that needed the exact search
+        }
         return;
       }
     }

@@ -42,10 +42,12 @@ def main():
         act.reverse()
         torch.cuda.synchronize()
         env.lib.bb_debug_counters(env.handle, buf.ctypes.data_as(C.c_void_p))
-        w = buf.reshape(-1)[: (n // epw) * 8].reshape(-1, 8)
-        tot = w.sum(axis=0).astype(np.float64)
+        w = buf.reshape(-1)[: (n // epw) * 9].reshape(-1, 9)
         lo = lambda v: float((v & np.uint64(0xFFFFFFFF)).astype(np.float64).sum())  # noqa: E731
         hi = lambda v: float((v >> np.uint64(32)).astype(np.float64).sum())  # noqa: E731
+        tot = w.sum(axis=0).astype(np.float64)
+        for c in (3, 4, 6):
+            tot[c] = lo(w[:, c])
         waves = w.shape[0]
         per = lambda x: round(x / waves / T, 1)  # noqa: E731  cycles per wave per step
         out.append({
@@ -57,6 +59,10 @@ def main():
             "attempts_per_search": round(tot[4] / max(tot[3], 1), 2),
             "passes_per_search": round(lo(w[:, 5]) / max(tot[3], 1), 2),
             "slow_passes_per_search": round(hi(w[:, 5]) / max(tot[3], 1), 2),
+            "slots_per_pass": round(hi(w[:, 6]) / max(lo(w[:, 5]), 1), 2),
+            "undecided_slots_per_search": round(hi(w[:, 3]) / max(tot[3], 1), 2),
+            "frac_first_attempt": round(hi(w[:, 4]) / max(tot[3], 1), 3),
+            "frac_first_attempt_quick": round(float(w[:, 8].astype(np.float64).sum()) / max(tot[3], 1), 3),
             "cyc_per_search": {"all": round(tot[1] / max(tot[3], 1)), "quick": round(tot[6] / max(tot[3], 1)),
                                "disjoint": round(lo(w[:, 7]) / max(tot[3], 1)),
                                "line": round(hi(w[:, 7]) / max(tot[3], 1))},

@@ -9,9 +9,9 @@ R=$GRAFT_REPO_ROOT
 cd /tmp || exit 1
 rocprofv3 -L > "$R/gpurun_out/${TAG}_counters.txt" 2>&1 || true
 i=0
-for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_IFETCH"; do
+for set in SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAVE_CYCLES,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY ${SETS:-SQC_ICACHE_MISSES,SQC_ICACHE_HITS,SQ_INSTS_SMEM,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_IFETCH}; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d "$R/gpurun_out/${TAG}_$i" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline --steps 30 --warmup 40 > "$R/gpurun_out/${TAG}_$i.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_$i.log"; echo "pass $i failed"; }
+  timeout -k 10 300 rocprofv3 --pmc ${set//,/ } --kernel-trace -d "$R/gpurun_out/${TAG}_$i" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline ${ARGS:---steps 30 --warmup 40} > "$R/gpurun_out/${TAG}_$i.log" 2>&1 || { tail -5 "$R/gpurun_out/${TAG}_$i.log"; echo "pass $i failed"; }
 done
 python - "$R/gpurun_out" "$TAG" <<'PY'
 import csv, glob, sys, collections
@@ -20,7 +20,7 @@ acc = collections.defaultdict(list)
 for f in glob.glob(f"{out}/{tag}_*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r.get("Kernel_Name", "")
-        for kn in ("step_kernel", "escalate_kernel"):
+        for kn in ("step_kernel", "escalate_kernel", "rollout_kernel"):
             if f"bb::{kn}(" in k:
                 acc[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (kn, c), v in sorted(acc.items()):
