@@ -578,12 +578,17 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
     for (int base = 0; base < total; base += 64) {
       const uint64_t tq0 = stats ? __builtin_amdgcn_s_memtime() : 0;
       const int slot = base + lane;
-      int j = 0;  // last packed attempt with e_off <= slot
-#pragma unroll
-      for (int step = 32; step > 0; step >>= 1) {
-        const int cand = j + step;
-        const int off = __shfl(e_off, cand < nb ? cand : 0);
-        if (cand < nb && off <= slot) j = cand;
+      // j = the packed attempt that owns this slot: each attempt marks its
+      // first slot of the pass in LDS, then a prefix max over the lanes
+      int j = 0;
+      if (nb > 1) {
+        wave_lds_fence();
+        lds[lane] = 0u;
+        wave_lds_fence();
+        if (lane < nb && S && e_off < base + 64 && e_off + (int)S > base)
+          atomicMax(&lds[e_off > base ? e_off - base : 0], (uint32_t)lane);
+        wave_lds_fence();
+        j = (int)wave_incl_max(lds[lane]);
       }
       const uint32_t jid = __shfl(e_ids, j);
       const uint64_t jA0 = __shfl(eA0, j), jA1 = __shfl(eA1, j), jA2 = __shfl(eA2, j);
