@@ -52,31 +52,41 @@ struct alignas(16) Tables {
 };
 static_assert(sizeof(PieceRow) % 16 == 0, "PieceRow staged as 16-byte vectors");
 
-// Global -> LDS copy of the piece rows and the |D| table as 16-byte vectors:
-// every load of a thread is issued before its first LDS store, so the
-// staging costs one memory latency (byte-wise copying cost ~22 serial ones).
-// The device buffers are padded (slab carving rounds to 256 bytes).
-__device__ __forceinline__ void stage_tables(Tables& t, const PieceRow* g_rows, const uint8_t* g_d) {
+// Global -> LDS copy of the piece rows and the |D| table (and, for the
+// kernels that run hand searches, the PCG64 jump-ahead table) as 16-byte
+// vectors: every load of a thread is issued before its first LDS store, so
+// the staging costs one memory latency (byte-wise copying cost ~22 serial
+// ones).  The device buffers are padded (slab carving rounds to 256 bytes).
+constexpr int kJumpVec = (kJumpMax + 1) * (int)sizeof(JumpRow) / 16;
+static_assert(sizeof(JumpRow) % 16 == 0, "JumpRow staged as 16-byte vectors");
+
+template <bool kWithJump = false>
+__device__ __forceinline__ void stage_tables(Tables& t, const PieceRow* g_rows, const uint8_t* g_d,
+                                             JumpRow* jt = nullptr, const JumpRow* g_jump = nullptr) {
   constexpr int kRowVec = kPieces * (int)sizeof(PieceRow) / 16;
-  constexpr int kTot = kRowVec + kDPad / 16;
+  constexpr int kTabVec = kRowVec + kDPad / 16;
+  constexpr int kTot = kTabVec + (kWithJump ? kJumpVec : 0);
   constexpr int kPer = (kTot + 63) / 64;
   const uint4* rs = reinterpret_cast<const uint4*>(g_rows);
   const uint4* ds = reinterpret_cast<const uint4*>(g_d);
+  const uint4* js = reinterpret_cast<const uint4*>(g_jump);
   uint4* rd = reinterpret_cast<uint4*>(t.row);
   uint4* dd = reinterpret_cast<uint4*>(t.d);
+  uint4* jd = reinterpret_cast<uint4*>(jt);
   const int tid = threadIdx.x;
   uint4 v[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int idx = tid + k * (int)blockDim.x;
-    if (idx < kTot) v[k] = idx < kRowVec ? rs[idx] : ds[idx - kRowVec];
+    if (idx < kTot) v[k] = idx < kRowVec ? rs[idx] : (idx < kTabVec ? ds[idx - kRowVec] : js[idx - kTabVec]);
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int idx = tid + k * (int)blockDim.x;
     if (idx < kTot) {
       if (idx < kRowVec) rd[idx] = v[k];
-      else dd[idx - kRowVec] = v[k];
+      else if (idx < kTabVec) dd[idx - kRowVec] = v[k];
+      else jd[idx - kTabVec] = v[k];
     }
   }
   __syncthreads();
@@ -488,7 +498,7 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
     s.cm = (int)((pr >> 24) & 0xFFu);
     s.gained = (int64_t)(uint32_t)(pr >> 32);
   }
-  stage_tables(t, g_rows, g_d);
+  stage_tables(t, g_rows, g_d);  // most escalate blocks find nothing parked: no jump table in LDS
   if (!parked) return;
   // one parked env at a time, searched by the whole wave (register broadcast)
   uint32_t my_ids = 0;
@@ -561,6 +571,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   __shared__ Tables t;
   __shared__ uint32_t scratch[kRollBlock];  // 64 words per wave (slow_phase_wave)
   uint32_t* lds = scratch + (threadIdx.x & ~63);
+  __shared__ JumpRow jt[kJumpMax + 1];
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * kRollBlock + threadIdx.x) >> 6;
   const int i = wave * kRollEnvs + lane;
@@ -592,7 +603,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     m[1] = e.mask[3 * i + 1];
     m[2] = e.mask[3 * i + 2];
   }
-  stage_tables(t, g_rows, g_d);
+  stage_tables<true>(t, g_rows, g_d, jt, a.jump);
   if (__ballot(live) == 0ull) return;  // wave-uniform
   if (live) s.rng.has = hand_has32(s.hand);
   const size_t N = (size_t)e.n;
@@ -645,7 +656,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       uint32_t ids = 0;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
       for (int q = 0; q < 12; ++q) st[q] = 0;
-      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, lds, st);
+      gen_hand_wave(wB, w, ids, 0, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds, st);
       dg[3] += 1 | ((uint64_t)st[9] << 32);
       dg[4] += st[0] | ((uint64_t)(st[0] == 1 ? 1u : 0u) << 32);
       dg[5] += st[1] | ((uint64_t)st[2] << 32);
@@ -653,7 +664,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       dg[7] += st[5] | ((uint64_t)st[6] << 32);
       dg[8] += (st[0] == 1 && st[10] == 0) ? 1u : 0u;
 #else
-      gen_hand_wave(wB, w, ids, 0, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next, lds);
+      gen_hand_wave(wB, w, ids, 0, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
 #endif
       if (lane == k) {
         s.rng = w;
