@@ -551,19 +551,29 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
 // sample_valid_actions -> step, with the Philox policy in place of
 // np.random.choice).
 // ---------------------------------------------------------------------------
+// Envs per wave: 32.  Lanes l and l + 32 both hold env l (identical state,
+// identical per-env instructions, stores from the lower half only): the
+// wave has two waves' worth of envs per SIMD at 65,536 envs, which hides the
+// LDS / dependent-ALU latency, and the mirrored halves split the in-lane
+// quick test of a new hand (each half tests its own fixed slots).  All 64
+// lanes join the wave-cooperative searches.
 #ifndef BB_ROLL_ENVS
 #define BB_ROLL_ENVS 32
 #endif
-// Envs per wave.  Fewer envs than lanes means more waves per SIMD (2 at
-// 65,536 envs with 32), which hides the LDS / dependent-ALU latency of the
-// searches; lanes >= kRollEnvs join the wave-cooperative searches only.
-constexpr int kRollEnvs = BB_ROLL_ENVS;
+constexpr int kRollEnvs = BB_ROLL_ENVS;  // 32 (two copies per env) or 16 (four)
+static_assert(kRollEnvs == 16 || kRollEnvs == 32, "envs per wave");
 #ifndef BB_ROLL_BLOCK
 #define BB_ROLL_BLOCK 64
 #endif
 constexpr int kRollBlock = BB_ROLL_BLOCK;
 #ifndef BB_ROLL_MINW
 #define BB_ROLL_MINW 1
+#endif
+#ifndef BB_MULTI
+#define BB_MULTI 1  // parked envs of a step searched together (gen_hands_multi); 0: one env at a time
+#endif
+#ifndef BB_ROLL_SLOTS
+#define BB_ROLL_SLOTS 1  // in-lane quick-test slots per copy (slot k = copy * this + 0, 1, ...)
 #endif
 
 __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
@@ -573,9 +583,11 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   uint32_t* lds = scratch + (threadIdx.x & ~63);
   __shared__ JumpRow jt[kJumpMax + 1];
   const int lane = threadIdx.x & 63;
+  const int half = lane / kRollEnvs;  // copy index; 0 = primary copy of the env (stores)
   const int wave = (blockIdx.x * kRollBlock + threadIdx.x) >> 6;
-  const int i = wave * kRollEnvs + lane;
-  const bool live = lane < kRollEnvs && i < e.n;
+  const int i = wave * kRollEnvs + (lane % kRollEnvs);
+  const bool live = i < e.n;
+  const bool primary = live && half == 0;
   StepCtx s;
   int act = 0;
   uint64_t m[3] = {0ull, 0ull, 0ull};
@@ -620,6 +632,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   for (int step = 0; step < r.steps; ++step) {
     BB_DIAG_T(c0);
     bool park = false;
+    Pcg after = s.rng;  // stream state after attempt 1's draws
     if (live) {
       if (apply_move(t, s, act)) {
         uint32_t ids = 0;
@@ -634,14 +647,44 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
           ids |= draw_piece(s.rng) << 12;
         }
 #else
-        park = !quick_hand(s.B, s.rng, ids, t.row, t.d, a.lane_quick);  // rolls back on failure
+        // draw attempt 1 (both halves identically); each half quick-tests its own slots
+        const Pcg save = s.rng;
+        const uint32_t x0 = draw_piece(s.rng);
+        const uint32_t x1 = draw_piece(s.rng);
+        const uint32_t x2 = draw_piece(s.rng);
+        ids = x0 | (x1 << 6) | (x2 << 12);
+        park = !quick_slots(s.B, x0, x1, x2, t.row, t.d, half * BB_ROLL_SLOTS, BB_ROLL_SLOTS);
+        after = s.rng;
+        s.rng = save;  // the wave search redraws the attempt unless a half accepts
 #endif
-        s.hand = ids | ((uint32_t)s.rng.has << 22);
+        s.hand = ids;
       }
     }
+    // accept if either copy accepted; else roll back for the wave search
+    uint64_t acc = ~__ballot(park) & __ballot(live && s.drew);
+    acc |= (acc >> kRollEnvs) | (acc << (64 - kRollEnvs));  // rotate: every copy sees the others
+    if (kRollEnvs == 16) acc |= (acc >> 32) | (acc << 32);
+    const bool accepted = (acc >> lane) & 1ull;
+    if (live && s.drew) {
+#if !defined(BB_ROLL_DIAG) || BB_ROLL_DIAG == 3
+      if (accepted) s.rng = after;
+      park = !accepted;
+#endif
+      s.hand = (s.hand & 0x3FFFFu) | ((uint32_t)s.rng.has << 22);
+    }
     // hand searches the in-lane test left open: the whole wave, one env at a time
-    uint64_t parked = __ballot(park);
+    uint64_t parked = __ballot(park) & ((1ull << kRollEnvs) - 1ull);
     BB_DIAG_T(c1);
+#if BB_MULTI
+    if (parked) {
+#if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
+      dg[3] += (uint64_t)__popcll(parked);
+#endif
+      uint32_t ids = 0;
+      gen_hands_multi<kRollEnvs>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+      if ((parked >> (lane % kRollEnvs)) & 1ull) s.hand = ids | ((uint32_t)s.rng.has << 22);
+    }
+#else
     while (parked) {
       const int k = __ffsll((unsigned long long)parked) - 1;
       parked &= parked - 1;
@@ -666,11 +709,12 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #else
       gen_hand_wave(wB, w, ids, 0, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
 #endif
-      if (lane == k) {
+      if ((lane % kRollEnvs) == k) {
         s.rng = w;
         s.hand = ids | ((uint32_t)w.has << 22);
       }
     }
+#endif
     BB_DIAG_T(c2);
     if (live) {
       masks_of(t, s.B, s.hand, m);
@@ -685,10 +729,12 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         term = over;
       }
       const size_t o = (size_t)step * N + (size_t)i;
-      r.reward[o] = (float)rew;
-      r.terminated[o] = term ? 1 : 0;
-      if (r.lines) r.lines[o] = (uint8_t)s.lines;
-      if (r.actions) r.actions[o] = act;
+      if (primary) {
+        r.reward[o] = (float)rew;
+        r.terminated[o] = term ? 1 : 0;
+        if (r.lines) r.lines[o] = (uint8_t)s.lines;
+        if (r.actions) r.actions[o] = act;
+      }
       if (term && a.autoreset) {  // wrappers.py:97-102
         reset_lane(t, s.has_seed, s.seed_hi, s.seed_lo, s.rng, s.B, s.hand, m);
         s.score = 0;
@@ -699,7 +745,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         s.blocks = 0;
         s.prev = 0;
       }
-      if (r.mask) {
+      if (r.mask && primary) {
         r.mask[3 * o + 0] = m[0];
         r.mask[3 * o + 1] = m[1];
         r.mask[3 * o + 2] = m[2];
@@ -717,7 +763,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   if (lane == 0 && a.dbg_out)
     for (int q = 0; q < 9; ++q) a.dbg_out[9 * wave + q] = dg[q];
 #endif
-  if (live) {
+  if (primary) {
     e.board[i] = s.B;
     e.hand[i] = s.hand;
     e.rng_hi[i] = s.rng.hi;

@@ -187,6 +187,33 @@ __device__ __forceinline__ int pair_quick(uint64_t B1, const PieceRow& pb, const
   return 2;
 }
 
+// Quick test of fixed level-1 slots k0 .. k0+slots-1 of the drawn hand
+// (x0, x1, x2) on B: slot k places piece k mod 3 at its lowest (k < 3) or
+// highest anchor, then pair_quick.  True on an accept (an exact success).
+__device__ __forceinline__ bool quick_slots(uint64_t B, uint32_t x0, uint32_t x1, uint32_t x2, const PieceRow* tbl,
+                                            const uint8_t* dtab, int k0, int slots) {
+  uint64_t A[3];
+  A[0] = anchors_of(tbl[x0], B);
+  A[1] = anchors_of(tbl[x1], B);
+  A[2] = anchors_of(tbl[x2], B);
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    if (kk >= slots) break;
+    const int k = k0 + kk;
+    const int f = k % 3;
+    const uint64_t Af = f == 0 ? A[0] : (f == 1 ? A[1] : A[2]);
+    if (!Af) continue;
+    const uint32_t fi = f == 0 ? x0 : (f == 1 ? x1 : x2);
+    const uint32_t bi = f == 0 ? x1 : x0;
+    const uint32_t ci = f == 2 ? x1 : x2;
+    const int p = k < 3 ? __ffsll((unsigned long long)Af) - 1 : 63 - __clzll((long long)Af);
+    const uint64_t B1 = clear_full(B | (tbl[fi].shape << p));
+    uint64_t A2, A3;
+    if (pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3) == 1) return true;
+  }
+  return false;
+}
+
 // In-lane quick test of the first attempt (step_kernel): draw its three
 // pieces and test up to `slots` fixed level-1 slots -- first piece f = k mod 3
 // at its lowest (k < 3) or highest anchor -- with pair_quick.  Straight-line
@@ -687,6 +714,192 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
   }
   ids = last_ids;  // 100 failures: the last hand is kept (engine.py:171-172)
   if (stats) stats[0] = (uint32_t)(attempt - attempt0);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative _generate_new_pieces for SEVERAL envs at once: the envs
+// parked in one rollout step.  Env e is held by lane e (and its copies in
+// lanes e + kEnvs, ...): board eB, stream rng; parked has bit e set for every
+// env to solve (e < kEnvs).  On return those lanes hold the final hand ids and stream state,
+// exactly the result of each env's own sequential loop.
+//
+// Each round draws a batch of attempts for every unsolved env by jump-ahead,
+// ATTEMPT-major (lane L = env slot L mod E, attempt L / E), so the leading
+// attempts -- the ones that usually decide -- of all envs share the first
+// pass.  Slots of the leading attempts that fit 64 lanes are tested as in
+// gen_hand_wave; an env accepts its earliest attempt with a successful slot
+// once every earlier attempt of its own is decided, else it advances past its
+// packed (all failed) attempts.  The first attempt lane is always packed, so
+// every round makes progress.
+// ---------------------------------------------------------------------------
+template <int kEnvs>
+__device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pcg& rng, uint32_t& ids,
+                                                const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
+                                                int lane, int pack_first, int pack_next, uint32_t* lds) {
+  const int me = lane % kEnvs;  // env index held by this lane
+  int att = 0;                // attempts consumed so far (env lanes)
+  uint32_t last_ids = 0;      // last drawn hand, kept after 100 failures (engine.py:171-172)
+  uint64_t todo = parked;
+  int round = 0;
+#pragma unroll 1
+  while (todo) {
+    const int E = __popcll(todo);
+    const int pk = round == 0 ? pack_first : pack_next;
+    int K = 64 / E;
+    K = K < pk ? K : pk;
+    K = K < kPack ? K : kPack;
+    K = K > 1 ? K : 1;
+    const int nl = E * K;
+    const int es = lane % E, k = lane / E;  // env slot, attempt offset of this lane
+    const int e = select_bit(todo, (uint32_t)es);
+    Pcg s0;
+    s0.hi = __shfl(rng.hi, e);
+    s0.lo = __shfl(rng.lo, e);
+    s0.inc_hi = __shfl(rng.inc_hi, e);
+    s0.inc_lo = __shfl(rng.inc_lo, e);
+    s0.buf = __shfl(rng.buf, e);
+    s0.has = __shfl((int)rng.has, e) != 0;
+    const uint64_t B = __shfl(eB, e);
+    const int a0 = __shfl(att, e);
+    const bool valid = lane < nl && a0 + k < kMaxAttempts;
+    uint32_t e_ids = 0;
+    Pcg e_after = s0;
+    bool rej = false;
+    if (valid) rej = draw_attempt_jump(s0, J, k, e_ids, e_after);
+    if (__ballot(rej)) {
+      // rare Lemire rejection: the lowest env on the exact sequential path
+      const int e0 = __ffsll((unsigned long long)todo) - 1;
+      Pcg w;
+      w.hi = __shfl(rng.hi, e0);
+      w.lo = __shfl(rng.lo, e0);
+      w.inc_hi = __shfl(rng.inc_hi, e0);
+      w.inc_lo = __shfl(rng.inc_lo, e0);
+      w.buf = __shfl(rng.buf, e0);
+      w.has = __shfl((int)rng.has, e0) != 0;
+      uint32_t wids = (uint32_t)__shfl((int)last_ids, e0);
+      gen_hand_wave(__shfl(eB, e0), w, wids, __shfl(att, e0), tbl, dtab, J, lane, pk, pack_next, lds);
+      if (me == e0) {
+        rng = w;
+        ids = wids;
+      }
+      todo &= todo - 1;
+      continue;
+    }
+    uint64_t eA0 = 0ull, eA1 = 0ull, eA2 = 0ull;
+    if (valid) {
+      eA0 = anchors_of(tbl[hand_id(e_ids, 0)], B);
+      eA1 = anchors_of(tbl[hand_id(e_ids, 1)], B);
+      eA2 = anchors_of(tbl[hand_id(e_ids, 2)], B);
+    }
+    const uint32_t S = valid ? (uint32_t)(__popcll(eA0) + __popcll(eA1) + __popcll(eA2)) : 0u;
+    const uint32_t incl = wave_incl_add(S);
+    const int e_off = (int)(incl - S);
+    int nb = __popcll(__ballot(lane < nl && incl <= 64u));  // leading attempt lanes that fit one pass
+    if (nb == 0) nb = 1;
+    const uint64_t packed = (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)) & __ballot(valid);
+    const int total = __builtin_amdgcn_readlane((int)incl, nb - 1);
+    uint64_t every = 0ull;  // bits 0, E, 2E, ...: the lanes of env slot 0
+    for (int L = 0; L < 64; L += E) every |= 1ull << L;
+    uint64_t okm = 0ull;  // attempt lanes with a successful slot
+#pragma unroll 1
+    for (int base = 0; base < total; base += 64) {
+      const int slot = base + lane;
+      int j = 0;
+      if (nb > 1) {
+        wave_lds_fence();
+        lds[lane] = 0u;
+        wave_lds_fence();
+        if (lane < nb && S && e_off < base + 64 && e_off + (int)S > base)
+          atomicMax(&lds[e_off > base ? e_off - base : 0], (uint32_t)lane);
+        wave_lds_fence();
+        j = (int)wave_incl_max(lds[lane]);
+      }
+      const uint32_t jid = __shfl(e_ids, j);
+      const uint64_t jA0 = __shfl(eA0, j), jA1 = __shfl(eA1, j), jA2 = __shfl(eA2, j);
+      const uint64_t jB = __shfl(B, j);
+      const int joff = __shfl(e_off, j);
+      int q = 0;
+      uint64_t B1 = 0, A2 = 0, A3 = 0;
+      uint32_t bi = 0, ci = 0;
+      if (slot < total) {
+        int rem = slot - joff;
+        const int c0 = __popcll(jA0), c1 = __popcll(jA1);
+        int f;
+        uint64_t Af;
+        if (rem < c0) {
+          f = 0;
+          Af = jA0;
+        } else if (rem < c0 + c1) {
+          f = 1;
+          Af = jA1;
+          rem -= c0;
+        } else {
+          f = 2;
+          Af = jA2;
+          rem -= c0 + c1;
+        }
+        const int p = select_bit(Af, (uint32_t)rem);
+        bi = hand_id(jid, f == 0 ? 1 : 0);
+        ci = hand_id(jid, f == 2 ? 1 : 2);
+        B1 = clear_full(jB | (tbl[hand_id(jid, f)].shape << p));
+        q = pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
+      }
+      // attempt lanes with a quick accept
+      wave_lds_fence();
+      lds[lane] = 0u;
+      wave_lds_fence();
+      if (q == 1) lds[j] = 1u;
+      wave_lds_fence();
+      const uint64_t qam = __ballot(lds[lane] != 0u);
+      // exact search only where no attempt of the same env up to this one accepted already
+      const uint64_t jenv = every << (j % E);
+      bool ok = q == 1;
+      const bool need = q == 2 && !(qam & jenv & ((2ull << j) - 1ull));
+      if (__ballot(need)) ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds);
+      wave_lds_fence();
+      lds[lane] = 0u;
+      wave_lds_fence();
+      if (ok) lds[j] = 1u;
+      wave_lds_fence();
+      okm |= __ballot(lds[lane] != 0u);
+      if (okm) break;  // more than one pass only for a single attempt lane: decided
+    }
+    // resolve every env of the round in its own lanes
+    const bool mine = (todo >> me) & 1ull;
+    const int my_es = __popcll(todo & ((1ull << me) - 1ull));
+    const uint64_t em = mine ? (every << my_es) & packed : 0ull;  // my env's packed attempt lanes
+    const uint64_t hit = em & okm;
+    int src = -1;
+    if (hit) src = __ffsll((unsigned long long)hit) - 1;  // earliest successful attempt
+    else if (em) src = 63 - __clzll((long long)em);        // last packed (all failed)
+    const int from = src < 0 ? lane : src;
+    const uint32_t f_ids = __shfl(e_ids, from);
+    Pcg fa;
+    fa.hi = __shfl(e_after.hi, from);
+    fa.lo = __shfl(e_after.lo, from);
+    fa.buf = __shfl(e_after.buf, from);
+    fa.has = __shfl((int)e_after.has, from) != 0;
+    bool done = false;
+    if (src >= 0) {
+      rng.hi = fa.hi;
+      rng.lo = fa.lo;
+      rng.buf = fa.buf;
+      rng.has = fa.has;
+      if (hit) {
+        ids = f_ids;
+        done = true;
+      } else {
+        att += __popcll(em);
+        last_ids = f_ids;
+        if (att >= kMaxAttempts) {
+          ids = last_ids;
+          done = true;
+        }
+      }
+    }
+    todo &= ~(__ballot(done && lane < kEnvs) & ((1ull << kEnvs) - 1ull));
+    ++round;
+  }
 }
 
 }  // namespace bb

@@ -13,7 +13,7 @@ for cfg in ${CFGS:-step:1 rollout:10 rollout:50 rollout:200}; do
   python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_$1_$2.json'));print('$1 T=$2', d['value'], d['roofline']['kernel_avg_ms'])"
 done
 for lib in ${LIBS:-}; do
-  for T in 50 200; do
+  for T in ${LTS:-128}; do
     BBVEC_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --mode rollout --rollout-len $T --steps 400 --warmup 40 > gpurun_out/bench_${TAG}_x.json 2>>gpurun_out/bench_${TAG}.err || exit 1
     python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_x.json'));print('$lib T=$T', d['value'], d['roofline']['kernel_avg_ms'])"
   done
