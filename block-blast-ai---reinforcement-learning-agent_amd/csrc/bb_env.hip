@@ -573,7 +573,10 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 #define BB_MULTI 1  // parked envs of a step searched together (gen_hands_multi); 0: one env at a time
 #endif
 #ifndef BB_ROLL_SLOTS
-#define BB_ROLL_SLOTS 1  // in-lane quick-test slots per copy (slot k = copy * this + 0, 1, ...)
+#define BB_ROLL_SLOTS 1  // in-lane quick-test slots per copy
+#endif
+#ifndef BB_ROLL_KSTEP
+#define BB_ROLL_KSTEP BB_ROLL_SLOTS  // copy c tests slots c * KSTEP, c * KSTEP + 1, ...
 #endif
 
 __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
@@ -618,6 +621,15 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   stage_tables<true>(t, g_rows, g_d, jt, a.jump);
   if (__ballot(live) == 0ull) return;  // wave-uniform
   if (live) s.rng.has = hand_has32(s.hand);
+  // A seeded env re-seeds with seed_value on every reset (block_blast_env.py:212-215), so its
+  // post-reset hand, stream and mask are the same each episode: computed once, kept in registers.
+  Pcg rs = s.rng;
+  uint32_t r_hand = 0;
+  uint64_t rm[3] = {0ull, 0ull, 0ull};
+  if (live && s.has_seed) {
+    uint64_t B0;
+    reset_lane(t, true, s.seed_hi, s.seed_lo, rs, B0, r_hand, rm);
+  }
   const size_t N = (size_t)e.n;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3  // timing diagnostics: per-wave phase cycles (reference semantics)
   // move+quick, searches, finalize, #searches, attempts | 1-attempt searches << 32, passes | slow passes << 32,
@@ -653,7 +665,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         const uint32_t x1 = draw_piece(s.rng);
         const uint32_t x2 = draw_piece(s.rng);
         ids = x0 | (x1 << 6) | (x2 << 12);
-        park = !quick_slots(s.B, x0, x1, x2, t.row, t.d, half * BB_ROLL_SLOTS, BB_ROLL_SLOTS);
+        park = !quick_slots(s.B, x0, x1, x2, t.row, t.d, half * BB_ROLL_KSTEP, BB_ROLL_SLOTS);
         after = s.rng;
         s.rng = save;  // the wave search redraws the attempt unless a half accepts
 #endif
@@ -736,7 +748,19 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         if (r.actions) r.actions[o] = act;
       }
       if (term && a.autoreset) {  // wrappers.py:97-102
-        reset_lane(t, s.has_seed, s.seed_hi, s.seed_lo, s.rng, s.B, s.hand, m);
+        if (s.has_seed) {
+          s.B = 0ull;
+          s.hand = r_hand;
+          s.rng.hi = rs.hi;
+          s.rng.lo = rs.lo;
+          s.rng.buf = rs.buf;
+          s.rng.has = rs.has;
+          m[0] = rm[0];
+          m[1] = rm[1];
+          m[2] = rm[2];
+        } else {  // seed_value None: the stream continues across episodes
+          reset_lane(t, false, s.seed_hi, s.seed_lo, s.rng, s.B, s.hand, m);
+        }
         s.score = 0;
         s.combo = 0;
         s.max_combo = 0;

@@ -18,11 +18,19 @@ pytestmark = pytest.mark.gpu
 SEED = 0xB10C
 
 
-def _env(n, offset, cuda, autoreset=True):
+def _env(n, offset, cuda, autoreset=True, unseeded=False):
+    import ctypes as C
+
     from runtime.device_env import DeviceEnvBatch
 
     env = DeviceEnvBatch(n, seeds=[42 + offset + i for i in range(n)], device=cuda, env_offset=offset,
                          autoreset=autoreset)
+    if unseeded:  # every other env seed_value None: fixed raw PCG words, stream continues across resets
+        seeds = np.array([42 + offset + i for i in range(n)], dtype=np.uint64)
+        has = (np.arange(n) % 2 == 0).astype(np.uint8)
+        raw = np.random.default_rng(99).integers(0, 2 ** 63, size=(n, 4), dtype=np.int64).astype(np.uint64)
+        assert env.lib.bb_seed(env.handle, seeds.ctypes.data_as(C.c_void_p), has.ctypes.data_as(C.c_void_p),
+                               raw.ctypes.data_as(C.c_void_p)) == 0
     env.reset()
     mb = torch.zeros((n, 3), dtype=torch.int64, device=cuda)
     env.obs(mask_bits=mb)
@@ -31,8 +39,8 @@ def _env(n, offset, cuda, autoreset=True):
     return env, a0
 
 
-def _chained_steps(n, offset, steps, cuda, step0=0, warm=0, autoreset=True):
-    env, a = _env(n, offset, cuda, autoreset)
+def _chained_steps(n, offset, steps, cuda, step0=0, warm=0, autoreset=True, unseeded=False):
+    env, a = _env(n, offset, cuda, autoreset, unseeded)
     nxt = torch.zeros_like(a)
     for t in range(warm):
         env.step(a, next_action=nxt, policy_seed=SEED, policy_step=t + 1)
@@ -58,8 +66,8 @@ def _chained_steps(n, offset, steps, cuda, step0=0, warm=0, autoreset=True):
     return out, st
 
 
-def _rollout(n, offset, steps, cuda, step0=0, warm=0, splits=(None,), autoreset=True):
-    env, a = _env(n, offset, cuda, autoreset)
+def _rollout(n, offset, steps, cuda, step0=0, warm=0, splits=(None,), autoreset=True, unseeded=False):
+    env, a = _env(n, offset, cuda, autoreset, unseeded)
     nxt = torch.zeros_like(a)
     for t in range(warm):
         env.step(a, next_action=nxt, policy_seed=SEED, policy_step=t + 1)
@@ -121,6 +129,15 @@ def test_rollout_without_autoreset(cuda):
     ref = _chained_steps(n, 0, steps, cuda, autoreset=False)
     assert (ref[0]["reward"] == -10.0).any()
     _assert_same(ref, _rollout(n, 0, steps, cuda, autoreset=False))
+
+
+def test_rollout_unseeded_envs(cuda):
+    """seed_value None (half the envs): auto-reset continues the stream
+    instead of re-seeding (engine.py:137-138)."""
+    n, steps = 512, 150
+    ref = _chained_steps(n, 0, steps, cuda, unseeded=True)
+    assert ref[0]["terminated"][:, 1::2].any()
+    _assert_same(ref, _rollout(n, 0, steps, cuda, unseeded=True))
 
 
 def test_rollout_full_size(cuda):
