@@ -634,7 +634,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3  // timing diagnostics: per-wave phase cycles (reference semantics)
   // move+quick, searches, finalize, #searches, attempts | 1-attempt searches << 32, passes | slow passes << 32,
   // quick cycles | slots << 32, disjoint | line cycles << 32
-  uint64_t dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t dg[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [9..14]: gen_hands_multi phases
   uint32_t st[12];
 #define BB_DIAG_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
 #else
@@ -689,11 +689,14 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     BB_DIAG_T(c1);
 #if BB_MULTI
     if (parked) {
+      uint32_t ids = 0;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
       dg[3] += (uint64_t)__popcll(parked);
-#endif
-      uint32_t ids = 0;
+      gen_hands_multi<kRollEnvs>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds,
+                                 &dg[9]);
+#else
       gen_hands_multi<kRollEnvs>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+#endif
       if ((parked >> (lane % kRollEnvs)) & 1ull) s.hand = ids | ((uint32_t)s.rng.has << 22);
     }
 #else
@@ -785,7 +788,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   }
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
   if (lane == 0 && a.dbg_out)
-    for (int q = 0; q < 9; ++q) a.dbg_out[9 * wave + q] = dg[q];
+    for (int q = 0; q < 15; ++q) a.dbg_out[15 * wave + q] = dg[q];
 #endif
   if (primary) {
     e.board[i] = s.B;

@@ -735,7 +735,9 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
 template <int kEnvs>
 __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pcg& rng, uint32_t& ids,
                                                 const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
-                                                int lane, int pack_first, int pack_next, uint32_t* lds) {
+                                                int lane, int pack_first, int pack_next, uint32_t* lds,
+                                                uint64_t* prof = nullptr) {  // diagnostics: [6] cycle sums
+#define BB_MT(x) const uint64_t x = prof ? __builtin_amdgcn_s_memtime() : 0
   const int me = lane % kEnvs;  // env index held by this lane
   int att = 0;                // attempts consumed so far (env lanes)
   uint32_t last_ids = 0;      // last drawn hand, kept after 100 failures (engine.py:171-172)
@@ -743,6 +745,7 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
   int round = 0;
 #pragma unroll 1
   while (todo) {
+    BB_MT(p0);
     const int E = __popcll(todo);
     const int pk = round == 0 ? pack_first : pack_next;
     int K = 64 / E;
@@ -750,7 +753,10 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
     K = K < kPack ? K : kPack;
     K = K > 1 ? K : 1;
     const int nl = E * K;
-    const int es = lane % E, k = lane / E;  // env slot, attempt offset of this lane
+    // env slot, attempt offset of this lane: lane / E through the f32 reciprocal
+    // ((lane + 0.5) / E is >= 1/64 away from an integer, far above its error)
+    const int k = (int)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)E));
+    const int es = lane - k * E;
     const int e = select_bit(todo, (uint32_t)es);
     Pcg s0;
     s0.hi = __shfl(rng.hi, e);
@@ -785,6 +791,7 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       todo &= todo - 1;
       continue;
     }
+    BB_MT(p1);
     uint64_t eA0 = 0ull, eA1 = 0ull, eA2 = 0ull;
     if (valid) {
       eA0 = anchors_of(tbl[hand_id(e_ids, 0)], B);
@@ -798,11 +805,14 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
     if (nb == 0) nb = 1;
     const uint64_t packed = (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)) & __ballot(valid);
     const int total = __builtin_amdgcn_readlane((int)incl, nb - 1);
-    uint64_t every = 0ull;  // bits 0, E, 2E, ...: the lanes of env slot 0
-    for (int L = 0; L < 64; L += E) every |= 1ull << L;
+    uint64_t every = 1ull;  // bits 0, E, 2E, ...: the lanes of env slot 0
+    for (int w = E; w < 64; w <<= 1) every |= every << w;
     uint64_t okm = 0ull;  // attempt lanes with a successful slot
+    BB_MT(p2);
+    uint64_t pq = 0, ps = 0;
 #pragma unroll 1
     for (int base = 0; base < total; base += 64) {
+      BB_MT(q0);
       const int slot = base + lane;
       int j = 0;
       if (nb > 1) {
@@ -844,26 +854,26 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
         B1 = clear_full(jB | (tbl[hand_id(jid, f)].shape << p));
         q = pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
       }
-      // attempt lanes with a quick accept
-      wave_lds_fence();
-      lds[lane] = 0u;
-      wave_lds_fence();
-      if (q == 1) lds[j] = 1u;
-      wave_lds_fence();
-      const uint64_t qam = __ballot(lds[lane] != 0u);
+      // attempt lanes with a quick accept: attempt lane L owns the pass's slot
+      // bits [lo, hi) of any slot ballot
+      const int lo = e_off > base ? e_off - base : 0;
+      const int hi = e_off + (int)S - base < 64 ? e_off + (int)S - base : 64;
+      const uint64_t own = (lane < nb && hi > lo) ? ((hi - lo == 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo)
+                                                  : 0ull;
+      const uint64_t qam = __ballot((__ballot(q == 1) & own) != 0ull);
       // exact search only where no attempt of the same env up to this one accepted already
       const uint64_t jenv = every << (j % E);
       bool ok = q == 1;
       const bool need = q == 2 && !(qam & jenv & ((2ull << j) - 1ull));
+      BB_MT(q1);
       if (__ballot(need)) ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds);
-      wave_lds_fence();
-      lds[lane] = 0u;
-      wave_lds_fence();
-      if (ok) lds[j] = 1u;
-      wave_lds_fence();
-      okm |= __ballot(lds[lane] != 0u);
+      BB_MT(q2);
+      pq += q1 - q0;
+      ps += q2 - q1;
+      okm |= __ballot((__ballot(ok) & own) != 0ull);
       if (okm) break;  // more than one pass only for a single attempt lane: decided
     }
+    BB_MT(p3);
     // resolve every env of the round in its own lanes
     const bool mine = (todo >> me) & 1ull;
     const int my_es = __popcll(todo & ((1ull << me) - 1ull));
@@ -899,7 +909,17 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
     }
     todo &= ~(__ballot(done && lane < kEnvs) & ((1ull << kEnvs) - 1ull));
     ++round;
+    if (prof) {
+      BB_MT(p4);
+      prof[0] += p1 - p0;  // batch setup + jump draws
+      prof[1] += p2 - p1;  // anchors, prefix scan, packing
+      prof[2] += pq;       // pass: quick tests + flags
+      prof[3] += ps;       // pass: exact phase
+      prof[4] += (p3 - p2) - pq - ps;  // pass overhead (owner flags of ok)
+      prof[5] += p4 - p3;  // resolve
+    }
   }
+#undef BB_MT
 }
 
 }  // namespace bb

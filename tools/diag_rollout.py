@@ -42,7 +42,7 @@ def main():
         act.reverse()
         torch.cuda.synchronize()
         env.lib.bb_debug_counters(env.handle, buf.ctypes.data_as(C.c_void_p))
-        w = buf.reshape(-1)[: (n // epw) * 9].reshape(-1, 9)
+        w = buf.reshape(-1)[: (n // epw) * 15].reshape(-1, 15)
         lo = lambda v: float((v & np.uint64(0xFFFFFFFF)).astype(np.float64).sum())  # noqa: E731
         hi = lambda v: float((v >> np.uint64(32)).astype(np.float64).sum())  # noqa: E731
         tot = w.sum(axis=0).astype(np.float64)
@@ -53,6 +53,8 @@ def main():
         out.append({
             "call": call, "waves": waves, "T": T,
             "cyc_per_wave_step": {"move_quick": per(tot[0]), "search": per(tot[1]), "finalize": per(tot[2])},
+            "multi_search_per_wave_step": {k: per(tot[9 + q]) for q, k in enumerate(
+                ("setup_draw", "anchors_scan", "pass_quick", "pass_exact", "pass_flags", "resolve"))},
             "max_wave_total": int((w[:, 0] + w[:, 1] + w[:, 2]).max()),
             "mean_wave_total": float((w[:, 0] + w[:, 1] + w[:, 2]).astype(np.float64).mean()),
             "searches_per_wave_step": round(tot[3] / waves / T, 3),
