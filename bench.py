@@ -99,6 +99,8 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
                     help="rollout: bb_rollout, T fused env-steps per launch (default); step: one bb_step per env-step")
+    ap.add_argument("--shards", type=int, default=1,
+                    help="rollout mode: split the envs into this many handles, one HIP stream each")
     ap.add_argument("--rollout-len", type=int, default=128,
                     help="T, env-steps per bb_rollout launch (default 128 = the reference's PPO horizon n_steps)")
     args = ap.parse_args()
@@ -128,22 +130,29 @@ def main() -> None:
 
     n = args.envs
     offset = rank * n
-    env = DeviceEnvBatch(n, seeds=[42 + offset + i for i in range(n)], device=dev, env_offset=offset)
-    env.reset()
-    mbits = torch.zeros((n, 3), dtype=torch.int64, device=dev)
-    env.obs(mask_bits=mbits)
-    act = [torch.zeros(n, dtype=torch.int32, device=dev), torch.zeros(n, dtype=torch.int32, device=dev)]
-    env.random_actions(mbits, act[0], seed=POLICY_SEED, step=0)
-
-    step_idx = [0]
+    S = max(1, args.shards) if args.mode == "rollout" else 1
+    assert n % S == 0
+    ns = n // S
     T = max(1, args.rollout_len)
-    if args.mode == "rollout":
-        # per-step outputs of one launch, [T][N] (rewritten by every launch)
-        r_rew = torch.zeros((T, n), dtype=torch.float32, device=dev)
-        r_term = torch.zeros((T, n), dtype=torch.uint8, device=dev)
-        r_lines = torch.zeros((T, n), dtype=torch.uint8, device=dev)
-        r_act = torch.zeros((T, n), dtype=torch.int32, device=dev)
-        r_mask = torch.zeros((T, n, 3), dtype=torch.int64, device=dev)
+    shards = []  # (env batch, stream, action double buffer, per-step outputs of one launch)
+    for k in range(S):
+        off = offset + k * ns
+        e = DeviceEnvBatch(ns, seeds=[42 + off + i for i in range(ns)], device=dev, env_offset=off)
+        e.reset()
+        mb = torch.zeros((ns, 3), dtype=torch.int64, device=dev)
+        e.obs(mask_bits=mb)
+        a = [torch.zeros(ns, dtype=torch.int32, device=dev), torch.zeros(ns, dtype=torch.int32, device=dev)]
+        e.random_actions(mb, a[0], seed=POLICY_SEED, step=0)
+        outs = None
+        if args.mode == "rollout":  # [T][N] (rewritten by every launch)
+            outs = (torch.zeros((T, ns), dtype=torch.float32, device=dev),
+                    torch.zeros((T, ns), dtype=torch.uint8, device=dev),
+                    torch.zeros((T, ns), dtype=torch.uint8, device=dev),
+                    torch.zeros((T, ns), dtype=torch.int32, device=dev),
+                    torch.zeros((T, ns, 3), dtype=torch.int64, device=dev))
+        shards.append((e, torch.cuda.Stream(dev) if S > 1 else torch.cuda.current_stream(dev), a, outs))
+    env, _, act, _ = shards[0]
+    step_idx = [0]
 
     def one_step(k=1):
         t = step_idx[0]
@@ -153,13 +162,20 @@ def main() -> None:
                          policy_step=t + j + 1)
             step_idx[0] = t + k
             return
+        cur = torch.cuda.current_stream(dev)
+        for _, st, _, _ in shards:
+            st.wait_stream(cur)
         done = 0
         while done < k:  # T steps per launch, the action double-buffer flips once per launch
             c = min(T, k - done)
-            env.rollout(c, act[0], r_rew, r_term, lines=r_lines, actions_out=r_act, mask_out=r_mask,
-                        next_action=act[1], policy_seed=POLICY_SEED, policy_step0=t + done)
-            act.reverse()
+            for e, st, a, (o_rew, o_term, o_lines, o_act, o_mask) in shards:
+                with torch.cuda.stream(st):
+                    e.rollout(c, a[0], o_rew, o_term, lines=o_lines, actions_out=o_act, mask_out=o_mask,
+                              next_action=a[1], policy_seed=POLICY_SEED, policy_step0=t + done)
+                a.reverse()
             done += c
+        for _, st, _, _ in shards:
+            cur.wait_stream(st)
         step_idx[0] = t + k
 
     one_step(args.warmup)
@@ -188,8 +204,9 @@ def main() -> None:
         el, kern_ms = float(t[0]), float(t[1])
 
     # sanity: every sampled action was legal -> no -10 rewards in the last step
-    last_rew = env.reward if args.mode == "step" else r_rew
-    assert bool((last_rew != -10.0).all()), "random policy produced an illegal action"
+    for e, _, _, outs in shards:
+        last_rew = e.reward if args.mode == "step" else outs[0]
+        assert bool((last_rew != -10.0).all()), "random policy produced an illegal action"
 
     total_env_steps = n * world * args.steps
     value = total_env_steps / el
@@ -236,7 +253,8 @@ def main() -> None:
             cb = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
-    env.close()
+    for e, _, _, _ in shards:
+        e.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -569,6 +569,9 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 #ifndef BB_ROLL_MINW
 #define BB_ROLL_MINW 1
 #endif
+#ifndef BB_ROLL_FAIR
+#define BB_ROLL_FAIR 2  // 1: alternate s_setprio between a SIMD's two waves every step; 2: behind one first
+#endif
 #ifndef BB_MULTI
 #define BB_MULTI 1  // parked envs of a step searched together (gen_hands_multi); 0: one env at a time
 #endif
@@ -634,14 +637,42 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3  // timing diagnostics: per-wave phase cycles (reference semantics)
   // move+quick, searches, finalize, #searches, attempts | 1-attempt searches << 32, passes | slow passes << 32,
   // quick cycles | slots << 32, disjoint | line cycles << 32
-  uint64_t dg[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [9..14]: gen_hands_multi phases
+  // [9..14]: gen_hands_multi phases, [15]: HW_ID | XCC_ID << 32, [16]: wave start, [17]: wave end
+  uint64_t dg[18] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  dg[15] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+           ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+  dg[16] = __builtin_amdgcn_s_memrealtime();  // 100 MHz, comparable across CUs
   uint32_t st[12];
 #define BB_DIAG_T(x) const uint64_t x = __builtin_amdgcn_s_memtime()
 #else
 #define BB_DIAG_T(x)
 #endif
+  // The two waves on a SIMD issue by priority, then age: the older one runs
+  // nearly unimpeded and the younger one finishes up to 1.3x later, which
+  // sets the launch time.  They alternate the higher priority every step
+  // (HW_ID wave slot parity differs between the two).
+  const uint32_t hwid = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+  const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // XCC_ID
+  const uint32_t wslot = hwid & 15u;
+  const uint32_t simd_key = (xcc << 12) | ((hwid >> 4) & 0xFFFu);
+  uint32_t* my_prog = r.prog + simd_key * 16u + wslot;
+  const uint32_t* partner_prog = r.prog + simd_key * 16u + (wslot ^ 1u);
+  uint32_t partner = 0;
 #pragma unroll 1
   for (int step = 0; step < r.steps; ++step) {
+#if BB_ROLL_FAIR == 1
+    if (((uint32_t)step ^ wslot) & 1u) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#elif BB_ROLL_FAIR == 2
+    {  // the wave behind its SIMD partner (global step counters) takes the priority
+      const uint32_t mine = (uint32_t)(r.policy_step0 + (uint64_t)step);
+      const int32_t lead = (int32_t)(mine - partner);
+      if (lead < 0 || (lead == 0 && (((uint32_t)step ^ wslot) & 1u))) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+      if (lane == 0) __hip_atomic_store(my_prog, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      partner = __hip_atomic_load(partner_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // used next step
+    }
+#endif
     BB_DIAG_T(c0);
     bool park = false;
     Pcg after = s.rng;  // stream state after attempt 1's draws
@@ -787,8 +818,9 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #endif
   }
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
+  dg[17] = __builtin_amdgcn_s_memrealtime();
   if (lane == 0 && a.dbg_out)
-    for (int q = 0; q < 15; ++q) a.dbg_out[15 * wave + q] = dg[q];
+    for (int q = 0; q < 18; ++q) a.dbg_out[18 * wave + q] = dg[q];
 #endif
   if (primary) {
     e.board[i] = s.B;

@@ -22,3 +22,12 @@ for kv in ${EXTRA:-}; do
   env $kv timeout -k 10 200 python bench.py --no-cpu-baseline --mode rollout --rollout-len 200 --steps 400 --warmup 40 > gpurun_out/bench_${TAG}_x.json 2>>gpurun_out/bench_${TAG}.err || exit 1
   python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_x.json'));print('$kv T=200', d['value'], d['roofline']['kernel_avg_ms'])"
 done
+for sh in ${SHARDS:-}; do
+  timeout -k 10 200 python bench.py --no-cpu-baseline --shards $sh --steps 1280 --warmup 128 > gpurun_out/bench_${TAG}_x.json 2>>gpurun_out/bench_${TAG}.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_x.json'));print('shards=$sh', d['value'], d['roofline']['kernel_avg_ms'])"
+done
+for cfg in ${SHT:-}; do
+  set -- ${cfg/:/ }
+  timeout -k 10 200 python bench.py --no-cpu-baseline --shards $1 --rollout-len $2 --steps 1280 --warmup 128 > gpurun_out/bench_${TAG}_x.json 2>>gpurun_out/bench_${TAG}.err || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_x.json'));print('shards=$1 T=$2', d['value'], d['roofline']['kernel_avg_ms'])"
+done
