@@ -225,18 +225,24 @@ class PPOAgent(BaseAgent):
         self.config = config or PPOConfig()
         self.network = BlockBlastNetwork(conv_channels=self.config.conv_channels,
                                          fc_hidden=self.config.fc_hidden).to(self.device)
-        self.optimizer = torch.optim.Adam(self.network.parameters(), lr=self.config.learning_rate, eps=1e-5)
+        # capturable: Adam's step count lives on the device, so the whole optimizer
+        # step can be replayed from a HIP graph (see train_minibatch)
+        self.optimizer = torch.optim.Adam(self.network.parameters(), lr=self.config.learning_rate, eps=1e-5,
+                                          capturable=self.device.type == "cuda")
         self.scheduler = None
         # Philox key for rollout sampling (derived from torch's seeded RNG)
         self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if sample_seed is None else int(sample_seed)
         self.sample_step = 0
         self._flat_grad = None
         self.autocast_dtype: Optional[torch.dtype] = None  # e.g. torch.bfloat16 for the CNN
+        # one optimizer step per minibatch replayed from a HIP graph (CUDA device, one process)
+        self.use_graphs = self.device.type == "cuda"
+        self._graphs = {}
 
     # ------------------------------------------------------------ helpers
     def _raw(self, x: torch.Tensor):
         if self.autocast_dtype is not None and x.is_cuda:
-            with torch.autocast("cuda", dtype=self.autocast_dtype):
+            with torch.autocast("cuda", dtype=self.autocast_dtype, cache_enabled=False):
                 logits, value = self.network.raw(x)
             return logits.float(), value.float()
         return self.network.raw(x)
@@ -342,6 +348,65 @@ class PPOAgent(BaseAgent):
         nn.utils.clip_grad_norm_(self.network.parameters(), self.config.max_grad_norm)
         self.optimizer.step()
 
+    def train_minibatch(self, x, masks, actions, old_log_probs, advantages, returns) -> torch.Tensor:
+        """One PPO optimizer step on a minibatch (ppo.py:362-401): loss, backward,
+        gradient all-reduce, clip, Adam.  Returns the 6 loss statistics on the
+        device.  On a single CUDA device the step is captured once per minibatch
+        shape into a HIP graph and replayed: a step is ~440 kernels, and issued
+        one by one from Python they left the GPU idle a third of the time."""
+        if not (self.use_graphs and x.is_cuda and _world() == 1):
+            loss, stats = self._minibatch_loss(x, masks, actions, old_log_probs, advantages, returns)
+            self._optimizer_step(loss)
+            return stats
+        inputs = (x, masks, actions, old_log_probs, advantages, returns)
+        key = (tuple(t.shape for t in inputs), self.autocast_dtype, self.network.training)
+        ent = self._graphs.get(key)
+        if ent is None:
+            ent = self._graphs[key] = self._capture_step(inputs)
+        graph, static_in, static_stats = ent
+        for dst, src in zip(static_in, inputs):
+            dst.copy_(src)
+        graph.replay()
+        return static_stats
+
+    def _capture_step(self, inputs):
+        """Capture one optimizer step.  The warm-up steps that graph capture
+        needs would change weights, BatchNorm statistics and Adam moments, so
+        those are snapshotted first and restored after the capture."""
+        static_in = [t.detach().clone() for t in inputs]
+        self._grad_buffer()
+        with torch.no_grad():
+            params = [p.detach().clone() for p in self.network.parameters()]
+            bufs = [b.detach().clone() for b in self.network.buffers()]
+            opt = {p: {k: v.detach().clone() for k, v in st.items() if torch.is_tensor(v)}
+                   for p, st in self.optimizer.state.items()}
+        dev_stream = torch.cuda.current_stream(self.device)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(dev_stream)
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                loss, _ = self._minibatch_loss(*static_in)
+                self._optimizer_step(loss)
+        dev_stream.wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            loss, stats = self._minibatch_loss(*static_in)
+            self._optimizer_step(loss)
+        with torch.no_grad():
+            for p, v in zip(self.network.parameters(), params):
+                p.copy_(v)
+            for b, v in zip(self.network.buffers(), bufs):
+                b.copy_(v)
+            for p, st in self.optimizer.state.items():
+                old = opt.get(p)
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        if old is not None and k in old:
+                            v.copy_(old[k])
+                        else:  # fresh Adam state == zero moments at step 0
+                            v.zero_()
+        return graph, static_in, stats
+
     def update(self, buffer, last_values, batch_size: Optional[int] = None) -> Dict[str, float]:
         """ppo.py:330-423.  Metrics are accumulated on the device and read once.
         ``batch_size`` overrides the per-rank minibatch (data-parallel runs
@@ -363,9 +428,7 @@ class PPOAgent(BaseAgent):
                     boards, pieces, masks, actions, old_lp, adv, ret = batch
                     x = BlockBlastNetwork.stack_input(boards.to(self.device), pieces.to(self.device))
                     masks, actions, old_lp, adv, ret = (t.to(self.device) for t in (masks, actions, old_lp, adv, ret))
-                loss, stats = self._minibatch_loss(x, masks, actions, old_lp, adv, ret)
-                self._optimizer_step(loss)
-                acc += stats
+                acc += self.train_minibatch(x, masks, actions, old_lp, adv, ret)
                 n += 1
         m = (acc / max(n, 1)).tolist()
         keys = ("policy_loss", "value_loss", "entropy", "total_loss", "approx_kl", "clip_fraction")
@@ -373,9 +436,12 @@ class PPOAgent(BaseAgent):
 
     # ----------------------------------------------------------- checkpoint
     def save(self, path: str) -> None:
-        """ppo.py:425-431 (same dict keys)."""
+        """ppo.py:425-431 (same dict keys).  Saved as a plain Adam (capturable
+        off), so the reference's own Adam loads it on any device."""
+        opt = self.optimizer.state_dict()
+        opt["param_groups"] = [dict(g, capturable=False) for g in opt["param_groups"]]
         torch.save({"network_state_dict": self.network.state_dict(),
-                    "optimizer_state_dict": self.optimizer.state_dict(),
+                    "optimizer_state_dict": opt,
                     "config": self.config.to_dict()}, path)
 
     def load(self, path: str) -> None:
@@ -384,6 +450,13 @@ class PPOAgent(BaseAgent):
         self.network.load_state_dict(ckpt["network_state_dict"])
         if "optimizer_state_dict" in ckpt:
             self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+            cap = self.device.type == "cuda"
+            for g in self.optimizer.param_groups:
+                g["capturable"] = cap
+            for st in self.optimizer.state.values():  # capturable Adam keeps its step count on the device
+                if "step" in st and torch.is_tensor(st["step"]):
+                    st["step"] = st["step"].to(self.device if cap else "cpu", torch.float32)
+        self._graphs = {}  # captured graphs reference the replaced optimizer state
         if "config" in ckpt:
             self.config = PPOConfig.from_dict(ckpt["config"])
         self._flat_grad = None

@@ -20,18 +20,44 @@ from torch.distributions import Categorical
 N_PARAMS_DEFAULT = 5_290_113  # parameter count of the default net
 
 
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d (same parameters, buffers and semantics) whose
+    training-mode forward/backward on the GPU are the HIP kernels of
+    csrc/bb_nn.hip, with the following ReLU fused when ``relu``.  Other modes
+    (eval, CPU, momentum=None) are nn.BatchNorm2d [+ ReLU] itself."""
+
+    use_fused = True
+
+    def __init__(self, num_features: int, relu: bool = False, **kw):
+        super().__init__(num_features, **kw)
+        self.fuse_relu = relu
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (self.use_fused and self.training and self.affine and self.track_running_stats
+                and self.momentum is not None):
+            from runtime.kernels import BatchNormReLUFunction, bn_fusable
+
+            if bn_fusable(x):
+                self.num_batches_tracked.add_(1)
+                return BatchNormReLUFunction.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                                   self.momentum, self.eps, self.fuse_relu)
+        y = super().forward(x)
+        return F.relu(y) if self.fuse_relu else y
+
+
 class ResidualBlock(nn.Module):
-    """network.py:14-30: conv-bn-relu-conv-bn + identity, relu."""
+    """network.py:14-30: conv-bn-relu-conv-bn + identity, relu (the first ReLU
+    fused into bn1)."""
 
     def __init__(self, channels: int):
         super().__init__()
         self.conv1 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
-        self.bn1 = nn.BatchNorm2d(channels)
+        self.bn1 = BatchNorm2d(channels, relu=True)
         self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
-        self.bn2 = nn.BatchNorm2d(channels)
+        self.bn2 = BatchNorm2d(channels)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = F.relu(self.bn1(self.conv1(x)))
+        y = self.bn1(self.conv1(x))
         y = self.bn2(self.conv2(y))
         return F.relu(y + x)
 
@@ -40,9 +66,11 @@ def _conv_stack(in_ch: int, channels: Sequence[int], batch_norm: bool, residual:
     layers = []
     for i, out_ch in enumerate(channels):
         layers.append(nn.Conv2d(in_ch, out_ch, kernel_size=3, padding=1))
-        if batch_norm:
-            layers.append(nn.BatchNorm2d(out_ch))
-        layers.append(nn.ReLU())
+        if batch_norm:  # ReLU fused into the BatchNorm; the Identity keeps the reference's module indices
+            layers.append(BatchNorm2d(out_ch, relu=True))
+            layers.append(nn.Identity())
+        else:
+            layers.append(nn.ReLU())
         if residual and i > 0:  # network.py:86-87
             layers.append(ResidualBlock(out_ch))
         in_ch = out_ch

@@ -105,3 +105,51 @@ def gather_obs(board: torch.Tensor, hand: torch.Tensor, mask_bits: torch.Tensor,
         "bb_gather_obs",
     )
     return x, mf
+
+
+# ---------------------------------------------------------------------------
+# Training-mode BatchNorm2d (+ fused ReLU) on the HIP kernels of csrc/bb_nn.hip
+# ---------------------------------------------------------------------------
+_BN_DTYPES = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def bn_fusable(x: torch.Tensor) -> bool:
+    """NCHW f32/bf16 device tensor whose HW rows are whole 16-byte vectors."""
+    return (x.is_cuda and x.dim() == 4 and x.dtype in _BN_DTYPES
+            and (x.shape[2] * x.shape[3] * x.element_size()) % 16 == 0 and x.numel() > 0)
+
+
+class BatchNormReLUFunction(torch.autograd.Function):
+    """y = [relu](batch_norm(x, batch statistics)) with running-stat update;
+    backward from x and the saved mean / inverse std (bb_bn_forward/backward)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool):
+        x = x.contiguous()
+        n, c, h, w = x.shape
+        dev = x.device
+        y = torch.empty_like(x)
+        ws = torch.empty(2 * c, dtype=torch.float64, device=dev)
+        mean = torch.empty(c, dtype=torch.float32, device=dev)
+        invstd = torch.empty(c, dtype=torch.float32, device=dev)
+        L.check(L.load().bb_bn_forward(_p(x), _BN_DTYPES[x.dtype], n, c, h * w, _p(weight), _p(bias), float(eps),
+                                       int(relu), _p(ws), _p(mean), _p(invstd), _p(running_mean), _p(running_var),
+                                       float(momentum), _p(y), _s(dev)), "bb_bn_forward")
+        ctx.save_for_backward(x, weight, bias, mean, invstd)
+        ctx.relu = bool(relu)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, mean, invstd = ctx.saved_tensors
+        dy = dy.contiguous().to(x.dtype)
+        n, c, h, w = x.shape
+        dev = x.device
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(weight)
+        db = torch.empty_like(bias)
+        ws = torch.empty(2 * c, dtype=torch.float64, device=dev)
+        L.check(L.load().bb_bn_backward(_p(x), _p(dy), _BN_DTYPES[x.dtype], n, c, h * w, _p(weight), _p(bias),
+                                        _p(mean), _p(invstd), int(ctx.relu), _p(ws), _p(dx), _p(dw), _p(db), _s(dev)),
+                "bb_bn_backward")
+        return dx, dw, db, None, None, None, None, None

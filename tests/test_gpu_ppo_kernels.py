@@ -106,3 +106,51 @@ def test_gather_obs_expansion(cuda):
     assert np.array_equal(x.cpu().numpy()[:, 1:], exp_pieces)
     bits = ((mbits.view(np.uint64)[idx][:, :, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1))
     assert np.array_equal(mf.cpu().numpy(), bits.reshape(-1, 192).astype(np.float32))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("n,c", [(2048, 128), (300, 64), (7, 4)])
+def test_fused_batchnorm_matches_torch(cuda, dtype, relu, n, c):
+    """models.network.BatchNorm2d (HIP bb_bn_forward/backward) vs
+    nn.BatchNorm2d [+ ReLU] in training mode: output, running statistics,
+    num_batches_tracked, dx / dweight / dbias.  fp32 within 1e-4 (reduction
+    order), bf16 within bf16 rounding of the output."""
+    from models.network import BatchNorm2d
+
+    torch.manual_seed(n + c)
+    x0 = (torch.randn(n, c, 8, 8, device=cuda) * 1.7 + 0.3).to(dtype)
+    ref = torch.nn.BatchNorm2d(c).to(cuda)
+    fus = BatchNorm2d(c, relu=relu).to(cuda)
+    with torch.no_grad():
+        w, b = torch.rand(c, device=cuda) + 0.5, torch.randn(c, device=cuda) * 0.1
+        for m in (ref, fus):
+            m.weight.copy_(w)
+            m.bias.copy_(b)
+    g = torch.randn(n, c, 8, 8, device=cuda).to(dtype)
+    # fused path
+    xf = x0.clone().requires_grad_(True)
+    yf = fus(xf)
+    yf.backward(g)
+    # reference (fp32 on the same values); with the ReLU, its backward takes the
+    # fused forward's own mask (ties at the kink may round either way)
+    xr = x0.float().clone().requires_grad_(True)
+    yr = ref(xr)
+    gr = g.float() * (yf.detach() > 0).float() if relu else g.float()
+    yr.backward(gr)
+    if relu:
+        yr = torch.relu(yr)
+    outs = [(yr.detach().float(), xr.grad.float(), ref.weight.grad, ref.bias.grad),
+            (yf.detach().float(), xf.grad.float(), fus.weight.grad, fus.bias.grad)]
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    for a, b_, name in zip(outs[0], outs[1], ("y", "dx", "dweight", "dbias")):
+        scale = max(1.0, float(a.abs().max()))
+        assert torch.allclose(a, b_, rtol=tol, atol=tol * scale), name
+    assert torch.allclose(ref.running_mean, fus.running_mean, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(ref.running_var, fus.running_var, rtol=1e-4, atol=1e-5)
+    assert int(ref.num_batches_tracked) == int(fus.num_batches_tracked) == 1
+    fus.eval()
+    ref.eval()
+    xe = x0.float()[:5]
+    ye = fus(xe)
+    assert torch.allclose(torch.relu(ref(xe)) if relu else ref(xe), ye, atol=1e-5)

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--autocast", choices=["none", "bf16"], default="none")
     ap.add_argument("--miopen-find", action="store_true", help="torch.backends.cudnn.benchmark = True")
     ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="issue the update step kernel by kernel")
     args = ap.parse_args()
 
     from agents import PPOAgent, PPOConfig
@@ -47,6 +48,7 @@ def main():
         agent.autocast_dtype = torch.bfloat16
     if args.channels_last:
         agent.network.to(memory_format=torch.channels_last)
+    agent.use_graphs = not args.no_graph
     agent.train()
     roll = DeviceRollout(args.envs, 0, args.envs, 42, {}, args.rollout, dev)
     roll.reset()
@@ -72,8 +74,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for x, m, a, lp, adv, ret in batches:
-        loss, _ = agent._minibatch_loss(x, m, a, lp, adv, ret)
-        agent._optimizer_step(loss)
+        agent.train_minibatch(x, m, a, lp, adv, ret)
         done += 1
         if done >= args.update_steps:
             break

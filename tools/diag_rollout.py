@@ -42,7 +42,7 @@ def main():
         act.reverse()
         torch.cuda.synchronize()
         env.lib.bb_debug_counters(env.handle, buf.ctypes.data_as(C.c_void_p))
-        w = buf.reshape(-1)[: (n // epw) * 15].reshape(-1, 15)
+        w = buf.reshape(-1)[: (n // epw) * 18].reshape(-1, 18)
         lo = lambda v: float((v & np.uint64(0xFFFFFFFF)).astype(np.float64).sum())  # noqa: E731
         hi = lambda v: float((v >> np.uint64(32)).astype(np.float64).sum())  # noqa: E731
         tot = w.sum(axis=0).astype(np.float64)
