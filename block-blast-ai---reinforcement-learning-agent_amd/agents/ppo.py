@@ -238,9 +238,21 @@ class PPOAgent(BaseAgent):
         # one optimizer step per minibatch replayed from a HIP graph (CUDA device, one process)
         self.use_graphs = self.device.type == "cuda"
         self._graphs = {}
+        self.channels_last = False
 
     # ------------------------------------------------------------ helpers
+    def set_channels_last(self, on: bool = True) -> None:
+        """Keep the conv stack's activations NHWC (torch.channels_last): MIOpen's
+        implicit-GEMM convolutions are NHWC kernels, so NCHW tensors are
+        transposed around every convolution; the BatchNorm kernels take both."""
+        self.channels_last = bool(on)
+        self.network.to(memory_format=torch.channels_last if on else torch.contiguous_format)
+        self._graphs = {}
+        self._flat_grad = None  # gradient views must follow the parameters' strides
+
     def _raw(self, x: torch.Tensor):
+        if self.channels_last and x.is_cuda:
+            x = x.contiguous(memory_format=torch.channels_last)
         if self.autocast_dtype is not None and x.is_cuda:
             with torch.autocast("cuda", dtype=self.autocast_dtype, cache_enabled=False):
                 logits, value = self.network.raw(x)
@@ -305,16 +317,19 @@ class PPOAgent(BaseAgent):
 
     # ------------------------------------------------------------- update
     def _grad_buffer(self) -> torch.Tensor:
-        """Flat fp32 gradient buffer; every parameter's .grad is a view into it,
-        so one all-reduce covers the whole model (5,290,113 floats)."""
+        """Flat fp32 gradient buffer for data-parallel runs; every parameter's
+        .grad is a view into it (same strides as the parameter, 256-byte
+        aligned so the accumulating adds stay vectorised), so one all-reduce
+        covers the whole model (5,290,113 floats plus alignment padding)."""
         if self._flat_grad is None:
             params = [p for p in self.network.parameters() if p.requires_grad]
-            n = sum(p.numel() for p in params)
-            self._flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
-            off = 0
+            offs, n = [], 0
             for p in params:
-                p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
-                off += p.numel()
+                offs.append(n)
+                n += -(-p.numel() // 64) * 64
+            self._flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
+            for p, off in zip(params, offs):
+                p.grad = torch.as_strided(self._flat_grad, p.size(), p.stride(), off)
         return self._flat_grad
 
     def _minibatch_loss(self, x, masks, actions, old_log_probs, advantages, returns):
@@ -338,13 +353,18 @@ class PPOAgent(BaseAgent):
         return loss, stats
 
     def _optimizer_step(self, loss: torch.Tensor) -> None:
-        flat = self._grad_buffer()
-        flat.zero_()
-        loss.backward()
         world = _world()
-        if world > 1:
+        if world > 1:  # one all-reduce (average) of the flat gradient buffer per optimizer step
+            flat = self._grad_buffer()
+            flat.zero_()
+            loss.backward()
             dist.all_reduce(flat)
             flat.div_(world)
+        else:  # autograd hands its gradient tensors over: no zero fill, no accumulating adds
+            self._flat_grad = None
+            for p in self.network.parameters():
+                p.grad = None
+            loss.backward()
         nn.utils.clip_grad_norm_(self.network.parameters(), self.config.max_grad_norm)
         self.optimizer.step()
 
@@ -374,7 +394,6 @@ class PPOAgent(BaseAgent):
         needs would change weights, BatchNorm statistics and Adam moments, so
         those are snapshotted first and restored after the capture."""
         static_in = [t.detach().clone() for t in inputs]
-        self._grad_buffer()
         with torch.no_grad():
             params = [p.detach().clone() for p in self.network.parameters()]
             bufs = [b.detach().clone() for b in self.network.buffers()]

@@ -503,38 +503,49 @@ int bb_gather_obs(const uint64_t* d_board, const uint32_t* d_hand, const uint64_
 }  // extern "C"
 
 namespace {
-int bn_check(int32_t dtype, int32_t N, int32_t C, int32_t HW) {
+int bn_check(int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW) {
   if (dtype != 0 && dtype != 1) return fail(nullptr, BB_ERR_ARG, "bb_bn: dtype must be 0 (f32) or 1 (bf16)");
+  if (nhwc != 0 && nhwc != 1) return fail(nullptr, BB_ERR_ARG, "bb_bn: layout must be 0 (NCHW) or 1 (NHWC)");
   if (N <= 0 || C <= 0 || HW <= 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: empty tensor");
-  if ((HW * (dtype == 1 ? 2 : 4)) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: HW rows must be 16-byte multiples");
+  const int esz = dtype == 1 ? 2 : 4;
+  if (!nhwc && (HW * esz) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: NCHW HW rows must be 16-byte multiples");
+  if (nhwc && ((C * esz) % 16 != 0 || 256 % (C * esz / 16) != 0))
+    return fail(nullptr, BB_ERR_ARG, "bb_bn: NHWC channel rows must be 16 B x a power of two <= 256");
   return BB_OK;
 }
 }  // namespace
 
-extern "C" int bb_bn_forward(const void* d_x, int32_t dtype, int32_t N, int32_t C, int32_t HW, const float* d_weight,
-                             const float* d_bias, float eps, int32_t relu, double* d_ws, float* d_save_mean,
-                             float* d_save_invstd, float* d_running_mean, float* d_running_var, float momentum,
-                             void* d_y, void* stream) {
-  int rc = bn_check(dtype, N, C, HW);
+extern "C" int64_t bb_bn_workspace_bytes(int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW) {
+  if (bn_check(dtype, nhwc, N, C, HW) != BB_OK) return -1;
+  return bn_workspace_bytes(dtype, nhwc, N, C, HW);
+}
+
+extern "C" int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW,
+                             const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps,
+                             int32_t relu, double* d_ws, float* d_save_mean, float* d_save_invstd,
+                             float* d_running_mean, float* d_running_var, float momentum, void* d_y, void* stream) {
+  int rc = bn_check(dtype, nhwc, N, C, HW);
   if (rc != BB_OK) return rc;
   if (!d_x || !d_weight || !d_bias || !d_ws || !d_save_mean || !d_save_invstd || !d_y)
     return fail(nullptr, BB_ERR_ARG, "bb_bn_forward: NULL argument");
-  hipError_t st = launch_bn_forward(d_x, dtype, N, C, HW, d_weight, d_bias, eps, relu, d_ws, d_save_mean,
-                                    d_save_invstd, d_running_mean, d_running_var, momentum, d_y, (hipStream_t)stream);
+  hipError_t st = launch_bn_forward(d_x, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
+                                    d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum, d_y,
+                                    (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_forward");
   return BB_OK;
 }
 
-extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t N, int32_t C, int32_t HW,
-                              const float* d_weight, const float* d_bias, const float* d_save_mean,
-                              const float* d_save_invstd, int32_t relu, double* d_ws, void* d_dx, float* d_dweight,
-                              float* d_dbias, void* stream) {
-  int rc = bn_check(dtype, N, C, HW);
+extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N, int32_t C,
+                              int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias,
+                              const float* d_save_mean, const float* d_save_invstd, int32_t relu, double* d_ws,
+                              void* d_dx, float* d_dweight, float* d_dbias, float* d_dpre_bias, void* stream) {
+  int rc = bn_check(dtype, nhwc, N, C, HW);
   if (rc != BB_OK) return rc;
   if (!d_x || !d_dy || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx)
     return fail(nullptr, BB_ERR_ARG, "bb_bn_backward: NULL argument");
-  hipError_t st = launch_bn_backward(d_x, d_dy, dtype, N, C, HW, d_weight, d_bias, d_save_mean, d_save_invstd, relu,
-                                     d_ws, d_dx, d_dweight, d_dbias, (hipStream_t)stream);
+  hipError_t st = launch_bn_backward(d_x, d_dy, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, d_save_mean,
+                                     d_save_invstd, relu, d_ws, d_dx, d_dweight, d_dbias, d_dpre_bias,
+                                     (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_backward");
   return BB_OK;
 }

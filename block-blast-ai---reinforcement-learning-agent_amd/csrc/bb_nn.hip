@@ -1,19 +1,25 @@
-// bb_nn.hip -- training-mode BatchNorm2d (+ fused ReLU) for the policy/value
-// CNN (gfx950).
+// bb_nn.hip -- training-mode BatchNorm2d (+ fused ReLU, + the preceding
+// convolution's bias) for the policy/value CNN (gfx950).
 //
 // BlockBlastNetwork's conv stack is conv -> BatchNorm2d -> ReLU on 8x8 boards
 // (network.py:75-117, ResidualBlock network.py:14-30).  With batch statistics
 // over N x 64 positions per channel, MIOpen's spatial BatchNorm took 80 us
 // forward and 200 us backward per layer at N = 2048 (bf16), about a third of a
-// PPO minibatch step; these kernels are HBM passes:
-//   forward : per-channel sum / sum of squares (fp32 lanes, fp64 block and
-//             global accumulation) -> normalise, scale, shift, optional ReLU,
-//             saved mean / inverse std, running-stat update (momentum,
-//             unbiased variance), exactly nn.BatchNorm2d's training forward;
-//   backward: per-channel sum(g) and sum(g * xhat) with g = dy masked by the
-//             ReLU (recomputed from x) -> dx, dweight, dbias.
-// Layout NCHW contiguous, f32 or bf16 activations, f32 parameters and stats.
-// Loads and stores are 16-byte vectors along HW (HW * element size % 16 == 0).
+// PPO minibatch step, and the convolution bias cost a separate add forward and
+// a reduction backward; these kernels are HBM passes:
+//   forward : u = x + conv_bias[c] (optional) -> per-channel sum / sum of
+//             squares -> normalise, scale, shift, optional ReLU, saved mean /
+//             inverse std, running-stat update (momentum, unbiased variance),
+//             exactly nn.BatchNorm2d's training forward of conv(x) + bias;
+//   backward: per-channel sum(g), sum(g * xhat), sum(xhat) with g = dy masked
+//             by the ReLU (recomputed from x) -> dx, dweight, dbias and the
+//             convolution bias gradient sum(dx).
+// Reductions are two-level without atomics: every block writes fp64 partials
+// (its rows, all its channels), one wave per channel adds them up in a fixed
+// order, so results are deterministic run to run.
+// Layout NCHW or NHWC (channels_last) contiguous, f32 or bf16 activations, f32
+// parameters and stats.  Loads and stores are 16-byte vectors along the
+// contiguous dimension (HW resp. C times the element size % 16 == 0).
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <math.h>
@@ -25,6 +31,8 @@ namespace bb {
 namespace {
 
 constexpr int kBnThreads = 256;
+constexpr int kUnroll = 4;  // rows in flight per thread in the NHWC reductions
+constexpr int kQ = 3;       // partial quantities per channel
 
 template <typename T>
 struct Vec;  // 16 bytes of T as floats
@@ -56,8 +64,8 @@ struct Vec<__hip_bfloat16> {
   }
   __device__ static uint32_t rne(float x) {  // f32 -> bf16 bits, round to nearest even (NaN kept quiet)
     const uint32_t u = __float_as_uint(x);
-    if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (u >> 16) | 0x40u;
-    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    const uint32_t r = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    return (u & 0x7FFFFFFFu) > 0x7F800000u ? ((u >> 16) | 0x40u) : r;  // a select, not a branch
   }
   __device__ static void store(void* p, int64_t i, const float* f) {
     uint4 v;
@@ -69,28 +77,163 @@ struct Vec<__hip_bfloat16> {
   }
 };
 
-__device__ __forceinline__ double block_sum(double v, double* red) {
+// Per-channel coefficients of the reduction passes (forward reads only pb).
+struct ChanCoef {
+  float pb, mu, is, sc, sh;
+};
+
+__device__ __forceinline__ ChanCoef coef_of(int c, const float* pre_bias, const float* mean, const float* invstd,
+                                            const float* w, const float* b, bool bwd) {
+  ChanCoef k;
+  k.pb = pre_bias ? pre_bias[c] : 0.f;
+  k.mu = bwd ? mean[c] : 0.f;
+  k.is = bwd ? invstd[c] : 0.f;
+  k.sc = bwd ? k.is * w[c] : 0.f;
+  k.sh = bwd ? b[c] : 0.f;
+  return k;
+}
+
+// One element's contribution: forward (u, u^2, 0); backward (g, g*xhat, xhat).
+template <bool BWD>
+__device__ __forceinline__ void accumulate(float xv, float gv, const ChanCoef& k, int relu, float& s, float& q,
+                                           float& t) {
+  const float u = xv + k.pb;
+  if (BWD) {
+    const float g = (relu && (u - k.mu) * k.sc + k.sh <= 0.f) ? 0.f : gv;  // the forward's exact ops
+    const float xh = (u - k.mu) * k.is;
+    s += g;
+    q += g * xh;
+    t += xh;
+  } else {
+    s += u;
+    q += u * u;
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[w] = v;
+  return v;
+}
+
+// NCHW reduction, block (c, s): channel c, images s, s + S, ... -> part[s][c][kQ].
+template <typename T, bool BWD>
+__global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restrict__ x, const void* __restrict__ dy,
+                                                             int N, int C, int HW, const float* __restrict__ pre_bias,
+                                                             const float* __restrict__ w, const float* __restrict__ b,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, int relu,
+                                                             double* __restrict__ part) {
+  __shared__ double red[kQ][kBnThreads / 64];
+  constexpr int V = Vec<T>::N;
+  const int c = blockIdx.x;
+  const int cpr = HW / V;  // 16-byte chunks per (n, c) row
+  const int rows_per_iter = kBnThreads / cpr;
+  const int r = threadIdx.x / cpr, kk = threadIdx.x % cpr;
+  const ChanCoef k = coef_of(c, pre_bias, mean, invstd, w, b, BWD);
+  float s = 0.f, q = 0.f, t = 0.f;
+  if (r < rows_per_iter) {
+    for (int n = blockIdx.y * rows_per_iter + r; n < N; n += gridDim.y * rows_per_iter) {
+      const int64_t i = ((int64_t)n * C + c) * cpr + kk;
+      float fx[V], fg[V];
+      Vec<T>::load(x, i, fx);
+      if (BWD) Vec<T>::load(dy, i, fg);
+#pragma unroll
+      for (int j = 0; j < V; ++j) accumulate<BWD>(fx[j], BWD ? fg[j] : 0.f, k, relu, s, q, t);
+    }
+  }
+  const double v[kQ] = {wave_sum((double)s), wave_sum((double)q), wave_sum((double)t)};
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int m = 0; m < kQ; ++m) red[m][wv] = v[m];
   __syncthreads();
-  double s = 0.0;
-  if (threadIdx.x == 0)
-    for (int k = 0; k < kBnThreads / 64; ++k) s += red[k];
-  return s;  // valid in thread 0
+  if (threadIdx.x < kQ) {
+    double a = 0.0;
+    for (int k2 = 0; k2 < kBnThreads / 64; ++k2) a += red[threadIdx.x][k2];
+    part[((int64_t)blockIdx.y * C + c) * kQ + threadIdx.x] = a;
+  }
+}
+
+// NHWC reduction: thread t owns the V channels of chunk t % cpr of rows
+// t / cpr, t / cpr + rows_per_iter, ... (cpr = C / V divides kBnThreads, so
+// its channels never change); block b writes part[b][c][kQ] for every c.
+template <typename T, bool BWD>
+__global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restrict__ x, const void* __restrict__ dy,
+                                                             int R, int C, const float* __restrict__ pre_bias,
+                                                             const float* __restrict__ w, const float* __restrict__ b,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, int relu,
+                                                             double* __restrict__ part) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float red[kQ][kBnThreads * V];
+  const int cpr = C / V;
+  const int rows_per_iter = kBnThreads / cpr;
+  const int r = threadIdx.x / cpr, kc = threadIdx.x % cpr;
+  ChanCoef k[V];
+  float s[V], q[V], t[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    k[j] = coef_of(kc * V + j, pre_bias, mean, invstd, w, b, BWD);
+    s[j] = q[j] = t[j] = 0.f;
+  }
+  const int stride = gridDim.x * rows_per_iter;
+  for (int n0 = blockIdx.x * rows_per_iter + r; n0 < R; n0 += kUnroll * stride) {
+    float fx[kUnroll][V], fg[kUnroll][BWD ? V : 1];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {  // all loads in flight before the arithmetic
+      const int n = n0 + u * stride;
+      if (n < R) {
+        Vec<T>::load(x, (int64_t)n * cpr + kc, fx[u]);
+        if (BWD) Vec<T>::load(dy, (int64_t)n * cpr + kc, fg[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (n0 + u * stride >= R) break;
+#pragma unroll
+      for (int j = 0; j < V; ++j) accumulate<BWD>(fx[u][j], BWD ? fg[u][j] : 0.f, k[j], relu, s[j], q[j], t[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    red[0][threadIdx.x * V + j] = s[j];
+    red[1][threadIdx.x * V + j] = q[j];
+    red[2][threadIdx.x * V + j] = t[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kBnThreads) {
+    const int cc = c / V, jc = c % V;
+    double a[kQ] = {0.0, 0.0, 0.0};
+    for (int rr = 0; rr < rows_per_iter; ++rr)
+      for (int m = 0; m < kQ; ++m) a[m] += red[m][(rr * cpr + cc) * V + jc];
+    for (int m = 0; m < kQ; ++m) part[((int64_t)blockIdx.x * C + c) * kQ + m] = a[m];
+  }
+}
+
+// sums[c][m] = sum over nb blocks of part[blk][c][m]: one wave per channel.
+__global__ void __launch_bounds__(kBnThreads) bn_sum_partials(const double* __restrict__ part, int nb, int C,
+                                                              double* __restrict__ sums) {
+  const int c = blockIdx.x * (kBnThreads / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double a[kQ] = {0.0, 0.0, 0.0};
+  for (int blk = lane; blk < nb; blk += 64)
+    for (int m = 0; m < kQ; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
+  for (int m = 0; m < kQ; ++m) a[m] = wave_sum(a[m]);
+  if (lane == 0)
+    for (int m = 0; m < kQ; ++m) sums[c * kQ + m] = a[m];
 }
 
 // Per-channel finalisation (one thread per channel): mean, inverse std of the
 // biased variance (the normalisation), running statistics with the unbiased
 // variance (nn.BatchNorm2d, momentum = exponential_average_factor).
-__global__ void bn_finalize_fwd(int C, double M, const double* __restrict__ ws, float eps,
+__global__ void bn_finalize_fwd(int C, double M, const double* __restrict__ sums, float eps,
                                 float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                 float* __restrict__ rmean, float* __restrict__ rvar, float momentum) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double m = ws[2 * c] / M;
-  double var = ws[2 * c + 1] / M - m * m;
+  const double m = sums[kQ * c] / M;
+  double var = sums[kQ * c + 1] / M - m * m;
   if (var < 0.0) var = 0.0;
   save_mean[c] = (float)m;
   save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
@@ -98,196 +241,218 @@ __global__ void bn_finalize_fwd(int C, double M, const double* __restrict__ ws, 
   if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1.0 ? var * M / (M - 1.0) : var);
 }
 
-// Block (c, s): channel c, images s, s + S, ...  ws[2c] += sum x, ws[2c+1] += sum x^2.
-template <typename T>
-__global__ void __launch_bounds__(kBnThreads) bn_reduce_fwd(const void* __restrict__ x, int N, int C, int HW,
-                                                            double* __restrict__ ws) {
-  __shared__ double red[2][kBnThreads / 64];
-  constexpr int V = Vec<T>::N;
-  const int c = blockIdx.x;
-  const int cpr = HW / V;  // 16-byte chunks per (n, c) row
-  const int rows_per_iter = kBnThreads / cpr;
-  const int r = threadIdx.x / cpr, k = threadIdx.x % cpr;
-  float s = 0.f, q = 0.f;
-  if (r < rows_per_iter) {
-    for (int n = blockIdx.y * rows_per_iter + r; n < N; n += gridDim.y * rows_per_iter) {
-      float f[V];
-      Vec<T>::load(x, ((int64_t)n * C + c) * cpr + k, f);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        s += f[j];
-        q += f[j] * f[j];
-      }
-    }
-  }
-  const double bs = block_sum((double)s, red[0]);
-  const double bq = block_sum((double)q, red[1]);
-  if (threadIdx.x == 0) {
-    atomicAdd(&ws[2 * c], bs);
-    atomicAdd(&ws[2 * c + 1], bq);
-  }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restrict__ x, void* __restrict__ y, int N,
-                                                           int C, int HW, const float* __restrict__ w,
-                                                           const float* __restrict__ b, int relu,
-                                                           const float* __restrict__ mean,
+// Channel of element j of 16-byte chunk i: NCHW rows are (n, c) with HW / V
+// chunks each (one channel per chunk); NHWC rows are (n, h, w) with C / V
+// chunks of V channels each.  The NHWC grid stride is a multiple of C / V, so
+// a thread's channels are fixed and their coefficients stay in registers.
+template <typename T, bool NHWC>
+__global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restrict__ x, void* __restrict__ y,
+                                                           int64_t total, int C, int cpr,
+                                                           const float* __restrict__ pre_bias,
+                                                           const float* __restrict__ w, const float* __restrict__ b,
+                                                           int relu, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd) {
   constexpr int V = Vec<T>::N;
-  const int cpr = HW / V;
-  const int64_t total = (int64_t)N * C * cpr;
-  for (int64_t i = (int64_t)blockIdx.x * kBnThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBnThreads) {
-    const int c = (int)((i / cpr) % C);
-    const float mu = mean[c], sc = invstd[c] * w[c], sh = b[c];
+  constexpr int NC = NHWC ? V : 1;
+  const int64_t g0 = (int64_t)blockIdx.x * kBnThreads + threadIdx.x;
+  float pb[NC], mu[NC], sc[NC], sh[NC];
+  auto load_coef = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      pb[j] = pre_bias ? pre_bias[c0 + j] : 0.f;
+      mu[j] = mean[c0 + j];
+      sc[j] = invstd[c0 + j] * w[c0 + j];
+      sh[j] = b[c0 + j];
+    }
+  };
+  if (NHWC) load_coef((int)(g0 % cpr) * V);
+  for (int64_t i = g0; i < total; i += (int64_t)gridDim.x * kBnThreads) {
+    if (!NHWC) load_coef((int)((i / cpr) % C));
     float f[V];
     Vec<T>::load(x, i, f);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const float v = (f[j] - mu) * sc + sh;
+      const int jc = NHWC ? j : 0;
+      const float v = (f[j] + pb[jc] - mu[jc]) * sc[jc] + sh[jc];
       f[j] = relu ? fmaxf(v, 0.f) : v;
     }
     Vec<T>::store(y, i, f);
   }
 }
 
-// ws[2c] += sum g, ws[2c+1] += sum g * xhat, g = dy (masked where the fused ReLU clipped).
-template <typename T>
-__global__ void __launch_bounds__(kBnThreads) bn_reduce_bwd(const void* __restrict__ x, const void* __restrict__ dy,
-                                                            int N, int C, int HW, const float* __restrict__ w,
-                                                            const float* __restrict__ b,
-                                                            const float* __restrict__ mean,
-                                                            const float* __restrict__ invstd, int relu,
-                                                            double* __restrict__ ws) {
-  __shared__ double red[2][kBnThreads / 64];
-  constexpr int V = Vec<T>::N;
-  const int c = blockIdx.x;
-  const int cpr = HW / V;
-  const int rows_per_iter = kBnThreads / cpr;
-  const int r = threadIdx.x / cpr, k = threadIdx.x % cpr;
-  const float mu = mean[c], is = invstd[c], sc = is * w[c], sh = b[c];
-  float s = 0.f, q = 0.f;
-  if (r < rows_per_iter) {
-    for (int n = blockIdx.y * rows_per_iter + r; n < N; n += gridDim.y * rows_per_iter) {
-      const int64_t i = ((int64_t)n * C + c) * cpr + k;
-      float fx[V], fg[V];
-      Vec<T>::load(x, i, fx);
-      Vec<T>::load(dy, i, fg);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const float g = (relu && (fx[j] - mu) * sc + sh <= 0.f) ? 0.f : fg[j];  // forward's exact ops
-        s += g;
-        q += g * (fx[j] - mu) * is;
-      }
-    }
-  }
-  const double bs = block_sum((double)s, red[0]);
-  const double bq = block_sum((double)q, red[1]);
-  if (threadIdx.x == 0) {
-    atomicAdd(&ws[2 * c], bs);
-    atomicAdd(&ws[2 * c + 1], bq);
-  }
-}
-
-template <typename T>
+template <typename T, bool NHWC>
 __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restrict__ x, const void* __restrict__ dy,
-                                                           void* __restrict__ dx, int N, int C, int HW,
+                                                           void* __restrict__ dx, int64_t total, int C, int cpr,
+                                                           double M, const float* __restrict__ pre_bias,
                                                            const float* __restrict__ w, const float* __restrict__ b,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd, int relu,
-                                                           const double* __restrict__ ws, float* __restrict__ dw,
-                                                           float* __restrict__ db) {
+                                                           const double* __restrict__ sums, float* __restrict__ dw,
+                                                           float* __restrict__ db, float* __restrict__ dpb) {
   constexpr int V = Vec<T>::N;
-  const int cpr = HW / V;
-  const int64_t total = (int64_t)N * C * cpr;
-  const float invM = (float)(1.0 / ((double)N * HW));
+  constexpr int NC = NHWC ? V : 1;
+  const float invM = (float)(1.0 / M);
   const int64_t g0 = (int64_t)blockIdx.x * kBnThreads + threadIdx.x;
   if (g0 < C) {
-    if (dw) dw[g0] = (float)ws[2 * g0 + 1];
-    if (db) db[g0] = (float)ws[2 * g0];
+    const int c = (int)g0;
+    const double sg = sums[kQ * c], sgx = sums[kQ * c + 1], sx = sums[kQ * c + 2];
+    if (dw) dw[c] = (float)sgx;
+    if (db) db[c] = (float)sg;
+    if (dpb) {  // sum over positions of dx = sc * (g - mg - xhat * mgx), evaluated in fp64
+      const double sc = (double)(invstd[c] * w[c]);
+      const double mg = (double)((float)sg * invM), mgx = (double)((float)sgx * invM);
+      dpb[c] = (float)(sc * (sg - M * mg) - sc * mgx * sx);
+    }
   }
+  float pb[NC], mu[NC], is[NC], sc[NC], sh[NC], mg[NC], mgx[NC];
+  auto load_coef = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int c = c0 + j;
+      pb[j] = pre_bias ? pre_bias[c] : 0.f;
+      mu[j] = mean[c];
+      is[j] = invstd[c];
+      sc[j] = is[j] * w[c];
+      sh[j] = b[c];
+      mg[j] = (float)sums[kQ * c] * invM;
+      mgx[j] = (float)sums[kQ * c + 1] * invM;
+    }
+  };
+  if (NHWC) load_coef((int)(g0 % cpr) * V);
   for (int64_t i = g0; i < total; i += (int64_t)gridDim.x * kBnThreads) {
-    const int c = (int)((i / cpr) % C);
-    const float mu = mean[c], is = invstd[c], sc = is * w[c], sh = b[c];
-    const float mg = (float)ws[2 * c] * invM, mgx = (float)ws[2 * c + 1] * invM;
+    if (!NHWC) load_coef((int)((i / cpr) % C));
     float fx[V], fg[V];
     Vec<T>::load(x, i, fx);
     Vec<T>::load(dy, i, fg);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const float g = (relu && (fx[j] - mu) * sc + sh <= 0.f) ? 0.f : fg[j];
-      const float xh = (fx[j] - mu) * is;
-      fx[j] = sc * (g - mg - xh * mgx);
+      const int jc = NHWC ? j : 0;
+      const float u = fx[j] + pb[jc];
+      const float g = (relu && (u - mu[jc]) * sc[jc] + sh[jc] <= 0.f) ? 0.f : fg[j];
+      const float xh = (u - mu[jc]) * is[jc];
+      fx[j] = sc[jc] * (g - mg[jc] - xh * mgx[jc]);
     }
     Vec<T>::store(dx, i, fx);
   }
 }
 
-int split_for(int N, int C, int HW, int V) {
-  // enough blocks per channel to fill the chip (>= 4 per CU overall), >= 4 rows per thread-row
-  const int rows_per_iter = kBnThreads / (HW / V);
-  int s = (1024 + C - 1) / C;
-  const int max_s = (N + rows_per_iter * 4 - 1) / (rows_per_iter * 4);
-  if (s > max_s) s = max_s;
-  if (s < 1) s = 1;
-  if (s > 65535) s = 65535;
-  return s;
+// ---------------------------------------------------------------- launch plan
+struct Plan {
+  int V, cpr, nb;  // vector width, 16-byte chunks per contiguous row, reduction blocks
+  dim3 rgrid;      // reduction grid
+  int64_t chunks;
+};
+
+Plan plan_for(int esz, int nhwc, int N, int C, int HW) {
+  Plan p;
+  p.V = 16 / esz;
+  p.chunks = (int64_t)N * C * HW / p.V;
+  if (nhwc) {
+    p.cpr = C / p.V;
+    const int rows_per_iter = kBnThreads / p.cpr;
+    const int64_t R = (int64_t)N * HW;
+    int64_t g = (R + (int64_t)rows_per_iter * kUnroll * 2 - 1) / ((int64_t)rows_per_iter * kUnroll * 2);
+    p.nb = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));  // >= 2 unrolled passes per thread
+    p.rgrid = dim3(p.nb);
+  } else {
+    p.cpr = HW / p.V;
+    const int rows_per_iter = kBnThreads / p.cpr;
+    int s = (1024 + C - 1) / C;  // enough blocks to fill the chip, >= 4 rows per thread-row
+    const int max_s = (N + rows_per_iter * 4 - 1) / (rows_per_iter * 4);
+    if (s > max_s) s = max_s;
+    if (s < 1) s = 1;
+    if (s > 65535) s = 65535;
+    p.nb = s;
+    p.rgrid = dim3(C, s);
+  }
+  return p;
 }
 
-int grid_for_elems(int64_t chunks) {
-  int64_t g = (chunks + kBnThreads - 1) / kBnThreads;
+// Elementwise grids: NHWC threads keep V channels' coefficients in registers,
+// so they stride over >= 8 chunks each to amortise loading them.
+int grid_for_elems(int64_t chunks, int nhwc) {
+  const int64_t per_thread = nhwc ? 8 : 1;
+  int64_t g = (chunks + kBnThreads * per_thread - 1) / (kBnThreads * per_thread);
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
   return (int)g;
 }
 
+template <typename T, bool BWD>
+void launch_reduce(const Plan& p, int nhwc, const void* x, const void* dy, int N, int C, int HW, const float* pb,
+                   const float* w, const float* b, const float* mean, const float* invstd, int relu, double* part,
+                   double* sums, hipStream_t s) {
+  if (nhwc)
+    hipLaunchKernelGGL((bn_reduce_nhwc<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N * HW, C, pb, w, b, mean,
+                       invstd, relu, part);
+  else
+    hipLaunchKernelGGL((bn_reduce_nchw<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N, C, HW, pb, w, b, mean,
+                       invstd, relu, part);
+  hipLaunchKernelGGL(bn_sum_partials, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, part, p.nb, C, sums);
+}
+
 template <typename T>
-hipError_t bn_forward_t(const void* x, int N, int C, int HW, const float* w, const float* b, float eps, int relu,
-                        double* ws, float* save_mean, float* save_invstd, float* rmean, float* rvar,
-                        float momentum, void* y, hipStream_t s) {
-  constexpr int V = Vec<T>::N;
-  hipError_t st = hipMemsetAsync(ws, 0, sizeof(double) * 2 * C, s);
-  if (st != hipSuccess) return st;
-  hipLaunchKernelGGL(bn_reduce_fwd<T>, dim3(C, split_for(N, C, HW, V)), dim3(kBnThreads), 0, s, x, N, C, HW, ws);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 255) / 256), dim3(256), 0, s, C, (double)N * HW, ws, eps, save_mean,
+hipError_t bn_forward_t(const void* x, int nhwc, int N, int C, int HW, const float* pb, const float* w,
+                        const float* b, float eps, int relu, double* ws, float* save_mean, float* save_invstd,
+                        float* rmean, float* rvar, float momentum, void* y, hipStream_t s) {
+  const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
+  double* sums = ws;
+  double* part = ws + kQ * C;
+  launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, part, sums, s);
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 255) / 256), dim3(256), 0, s, C, (double)N * HW, sums, eps, save_mean,
                      save_invstd, rmean, rvar, momentum);
-  hipLaunchKernelGGL(bn_apply_fwd<T>, dim3(grid_for_elems((int64_t)N * C * (HW / V))), dim3(kBnThreads), 0, s, x, y,
-                     N, C, HW, w, b, relu, save_mean, save_invstd);
+  const dim3 ge(grid_for_elems(p.chunks, nhwc));
+  if (nhwc)
+    hipLaunchKernelGGL((bn_apply_fwd<T, true>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, pb, w, b, relu,
+                       save_mean, save_invstd);
+  else
+    hipLaunchKernelGGL((bn_apply_fwd<T, false>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, pb, w, b,
+                       relu, save_mean, save_invstd);
   return hipGetLastError();
 }
 
 template <typename T>
-hipError_t bn_backward_t(const void* x, const void* dy, int N, int C, int HW, const float* w, const float* b,
-                         const float* mean, const float* invstd, int relu, double* ws, void* dx, float* dw, float* db,
-                         hipStream_t s) {
-  constexpr int V = Vec<T>::N;
-  hipError_t st = hipMemsetAsync(ws, 0, sizeof(double) * 2 * C, s);
-  if (st != hipSuccess) return st;
-  hipLaunchKernelGGL(bn_reduce_bwd<T>, dim3(C, split_for(N, C, HW, V)), dim3(kBnThreads), 0, s, x, dy, N, C, HW, w,
-                     b, mean, invstd, relu, ws);
-  const int64_t chunks = (int64_t)N * C * (HW / V);
-  hipLaunchKernelGGL(bn_apply_bwd<T>, dim3(grid_for_elems(chunks > C ? chunks : C)), dim3(kBnThreads), 0, s, x, dy,
-                     dx, N, C, HW, w, b, mean, invstd, relu, ws, dw, db);
+hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, int HW, const float* pb,
+                         const float* w, const float* b, const float* mean, const float* invstd, int relu, double* ws,
+                         void* dx, float* dw, float* db, float* dpb, hipStream_t s) {
+  const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
+  double* sums = ws;
+  double* part = ws + kQ * C;
+  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, part, sums, s);
+  const dim3 ge(grid_for_elems(p.chunks > C ? p.chunks : C, nhwc));
+  const double M = (double)N * HW;
+  if (nhwc)
+    hipLaunchKernelGGL((bn_apply_bwd<T, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, M, pb, w,
+                       b, mean, invstd, relu, sums, dw, db, dpb);
+  else
+    hipLaunchKernelGGL((bn_apply_bwd<T, false>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, M, pb, w,
+                       b, mean, invstd, relu, sums, dw, db, dpb);
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_bn_forward(const void* x, int dtype, int N, int C, int HW, const float* w, const float* b, float eps,
-                             int relu, double* ws, float* save_mean, float* save_invstd, float* rmean, float* rvar,
-                             float momentum, void* y, hipStream_t s) {
-  if (dtype == 1)
-    return bn_forward_t<__hip_bfloat16>(x, N, C, HW, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar,
-                                        momentum, y, s);
-  return bn_forward_t<float>(x, N, C, HW, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar, momentum, y, s);
+int64_t bn_workspace_bytes(int dtype, int nhwc, int N, int C, int HW) {
+  const Plan p = plan_for(dtype == 1 ? 2 : 4, nhwc, N, C, HW);
+  return (int64_t)sizeof(double) * kQ * C * (1 + (int64_t)p.nb);
 }
 
-hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int N, int C, int HW, const float* w,
-                              const float* b, const float* mean, const float* invstd, int relu, double* ws, void* dx,
-                              float* dw, float* db, hipStream_t s) {
+hipError_t launch_bn_forward(const void* x, int dtype, int nhwc, int N, int C, int HW, const float* pb,
+                             const float* w, const float* b, float eps, int relu, double* ws, float* save_mean,
+                             float* save_invstd, float* rmean, float* rvar, float momentum, void* y, hipStream_t s) {
   if (dtype == 1)
-    return bn_backward_t<__hip_bfloat16>(x, dy, N, C, HW, w, b, mean, invstd, relu, ws, dx, dw, db, s);
-  return bn_backward_t<float>(x, dy, N, C, HW, w, b, mean, invstd, relu, ws, dx, dw, db, s);
+    return bn_forward_t<__hip_bfloat16>(x, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean,
+                                        rvar, momentum, y, s);
+  return bn_forward_t<float>(x, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar, momentum,
+                             y, s);
+}
+
+hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
+                              const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
+                              int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s) {
+  if (dtype == 1)
+    return bn_backward_t<__hip_bfloat16>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s);
+  return bn_backward_t<float>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s);
 }
 
 }  // namespace bb

@@ -32,17 +32,58 @@ class BatchNorm2d(nn.BatchNorm2d):
         super().__init__(num_features, **kw)
         self.fuse_relu = relu
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if (self.use_fused and self.training and self.affine and self.track_running_stats
+    def fusable(self, x: torch.Tensor) -> bool:
+        if not (self.use_fused and self.training and self.affine and self.track_running_stats
                 and self.momentum is not None):
-            from runtime.kernels import BatchNormReLUFunction, bn_fusable
+            return False
+        from runtime.kernels import bn_fusable
 
-            if bn_fusable(x):
-                self.num_batches_tracked.add_(1)
-                return BatchNormReLUFunction.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                                   self.momentum, self.eps, self.fuse_relu)
+        return bn_fusable(x)
+
+    def forward(self, x: torch.Tensor, pre_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """BatchNorm2d(x + pre_bias) [-> ReLU]; ``pre_bias`` is a preceding
+        convolution's bias that was left out of the convolution."""
+        if self.fusable(x):
+            from runtime.kernels import BatchNormReLUFunction
+
+            self.num_batches_tracked.add_(1)
+            return BatchNormReLUFunction.apply(x, pre_bias, self.weight, self.bias, self.running_mean,
+                                               self.running_var, self.momentum, self.eps, self.fuse_relu)
+        if pre_bias is not None:
+            x = x + pre_bias.view(1, -1, 1, 1).to(x.dtype)
         y = super().forward(x)
         return F.relu(y) if self.fuse_relu else y
+
+
+def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """bn(conv(x)).  When the BatchNorm runs on the HIP kernels the
+    convolution's bias is added inside them (one add on load instead of a
+    separate pass, and its gradient comes out of the BatchNorm backward instead
+    of a reduction over dy)."""
+    if isinstance(bn, BatchNorm2d) and conv.bias is not None and bn.training and x.is_cuda and bn.use_fused:
+        z = conv._conv_forward(x, conv.weight, None)
+        if bn.fusable(z):
+            return bn(z, pre_bias=conv.bias)
+        return bn(z + conv.bias.view(1, -1, 1, 1).to(z.dtype))
+    return bn(conv(x))
+
+
+class ConvStack(nn.Sequential):
+    """nn.Sequential (same module indices, so the same state_dict keys) that
+    runs each Conv2d -> BatchNorm2d pair through conv_bn."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        mods = list(self)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if isinstance(m, nn.Conv2d) and i + 1 < len(mods) and isinstance(mods[i + 1], BatchNorm2d):
+                x = conv_bn(m, mods[i + 1], x)
+                i += 2
+                continue
+            x = m(x)
+            i += 1
+        return x
 
 
 class ResidualBlock(nn.Module):
@@ -57,8 +98,8 @@ class ResidualBlock(nn.Module):
         self.bn2 = BatchNorm2d(channels)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = self.bn1(self.conv1(x))
-        y = self.bn2(self.conv2(y))
+        y = conv_bn(self.conv1, self.bn1, x)
+        y = conv_bn(self.conv2, self.bn2, y)
         return F.relu(y + x)
 
 
@@ -74,7 +115,7 @@ def _conv_stack(in_ch: int, channels: Sequence[int], batch_norm: bool, residual:
         if residual and i > 0:  # network.py:86-87
             layers.append(ResidualBlock(out_ch))
         in_ch = out_ch
-    return nn.Sequential(*layers)
+    return ConvStack(*layers)
 
 
 def _mlp(in_f: int, hidden: Sequence[int]) -> nn.Sequential:

@@ -113,43 +113,70 @@ def gather_obs(board: torch.Tensor, hand: torch.Tensor, mask_bits: torch.Tensor,
 _BN_DTYPES = {torch.float32: 0, torch.bfloat16: 1}
 
 
+def _bn_layout(x: torch.Tensor) -> int:
+    """1 when x is laid out channels_last (NHWC) and not also NCHW-contiguous."""
+    return int(x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous())
+
+
 def bn_fusable(x: torch.Tensor) -> bool:
-    """NCHW f32/bf16 device tensor whose HW rows are whole 16-byte vectors."""
-    return (x.is_cuda and x.dim() == 4 and x.dtype in _BN_DTYPES
-            and (x.shape[2] * x.shape[3] * x.element_size()) % 16 == 0 and x.numel() > 0)
+    """f32/bf16 device tensor, NCHW with HW rows or NHWC with C rows of whole
+    16-byte vectors."""
+    if not (x.is_cuda and x.dim() == 4 and x.dtype in _BN_DTYPES and x.numel() > 0):
+        return False
+    if _bn_layout(x):
+        row = x.shape[1] * x.element_size()  # bytes per NHWC row: 16 x a power of two <= 256
+        return row % 16 == 0 and 256 % (row // 16) == 0
+    return (x.shape[2] * x.shape[3] * x.element_size()) % 16 == 0
+
+
+def _bn_workspace(x: torch.Tensor, nhwc: int) -> torch.Tensor:
+    n, c, h, w = x.shape
+    nbytes = L.load().bb_bn_workspace_bytes(_BN_DTYPES[x.dtype], nhwc, n, c, h * w)
+    if nbytes < 0:
+        raise L.BBNativeError(f"bb_bn_workspace_bytes rejected shape {tuple(x.shape)} {x.dtype} nhwc={nhwc}")
+    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=x.device)
 
 
 class BatchNormReLUFunction(torch.autograd.Function):
-    """y = [relu](batch_norm(x, batch statistics)) with running-stat update;
-    backward from x and the saved mean / inverse std (bb_bn_forward/backward)."""
+    """y = [relu](batch_norm(x + pre_bias, batch statistics)) with running-stat
+    update; backward from x and the saved mean / inverse std
+    (bb_bn_forward/backward).  ``pre_bias`` is the preceding convolution's
+    bias (None = none), so conv(x) without bias -> this == conv(x) + bias ->
+    nn.BatchNorm2d [-> ReLU]; its gradient is the per-channel sum of dx."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool):
-        x = x.contiguous()
+    def forward(ctx, x, pre_bias, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool):
+        nhwc = _bn_layout(x)
+        x = x.contiguous(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         n, c, h, w = x.shape
         dev = x.device
         y = torch.empty_like(x)
-        ws = torch.empty(2 * c, dtype=torch.float64, device=dev)
+        ws = _bn_workspace(x, nhwc)
         mean = torch.empty(c, dtype=torch.float32, device=dev)
         invstd = torch.empty(c, dtype=torch.float32, device=dev)
-        L.check(L.load().bb_bn_forward(_p(x), _BN_DTYPES[x.dtype], n, c, h * w, _p(weight), _p(bias), float(eps),
-                                       int(relu), _p(ws), _p(mean), _p(invstd), _p(running_mean), _p(running_var),
-                                       float(momentum), _p(y), _s(dev)), "bb_bn_forward")
-        ctx.save_for_backward(x, weight, bias, mean, invstd)
+        L.check(L.load().bb_bn_forward(_p(x), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight),
+                                       _p(bias), float(eps), int(relu), _p(ws), _p(mean), _p(invstd),
+                                       _p(running_mean), _p(running_var), float(momentum), _p(y), _s(dev)),
+                "bb_bn_forward")
+        ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd)
         ctx.relu = bool(relu)
+        ctx.nhwc = nhwc
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, bias, mean, invstd = ctx.saved_tensors
-        dy = dy.contiguous().to(x.dtype)
+        x, pre_bias, weight, bias, mean, invstd = ctx.saved_tensors
+        fmt = torch.channels_last if ctx.nhwc else torch.contiguous_format
+        dy = dy.to(x.dtype).contiguous(memory_format=fmt)
         n, c, h, w = x.shape
         dev = x.device
         dx = torch.empty_like(x)
         dw = torch.empty_like(weight)
         db = torch.empty_like(bias)
-        ws = torch.empty(2 * c, dtype=torch.float64, device=dev)
-        L.check(L.load().bb_bn_backward(_p(x), _p(dy), _BN_DTYPES[x.dtype], n, c, h * w, _p(weight), _p(bias),
-                                        _p(mean), _p(invstd), int(ctx.relu), _p(ws), _p(dx), _p(dw), _p(db), _s(dev)),
+        dpb = torch.empty_like(pre_bias) if pre_bias is not None else None
+        ws = _bn_workspace(x, ctx.nhwc)
+        L.check(L.load().bb_bn_backward(_p(x), _p(dy), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w, _p(pre_bias),
+                                        _p(weight), _p(bias), _p(mean), _p(invstd), int(ctx.relu), _p(ws), _p(dx),
+                                        _p(dw), _p(db), _p(dpb), _s(dev)),
                 "bb_bn_backward")
-        return dx, dw, db, None, None, None, None, None
+        return dx, dpb, dw, db, None, None, None, None, None

@@ -239,25 +239,34 @@ int bb_gather_obs(const uint64_t* d_board, const uint32_t* d_hand,
                   const uint64_t* d_mask_bits, const int64_t* d_index,
                   int32_t n, float* d_x, float* d_mask_f32, void* stream);
 
-/* Training-mode BatchNorm2d with an optional fused ReLU, NCHW, for the
- * policy/value CNN's conv stack (network.py:75-117 conv -> BatchNorm2d -> ReLU,
- * ResidualBlock network.py:14-30).  dtype 0 = f32, 1 = bf16 activations;
- * weight / bias / statistics are f32; HW * element size must be a multiple of
- * 16 bytes.  Forward = nn.BatchNorm2d training forward (batch mean, biased
- * variance for the normalisation; running_mean / running_var updated with
- * `momentum` and the unbiased variance when non-NULL), then max(y, 0) if relu.
- * d_ws is caller scratch of 2*C doubles.  Backward takes the forward's input x
- * and saved mean / inverse std; with relu it recomputes the mask from x. */
-int bb_bn_forward(const void* d_x, int32_t dtype, int32_t N, int32_t C, int32_t HW,
-                  const float* d_weight, const float* d_bias, float eps, int32_t relu,
-                  double* d_ws, float* d_save_mean, float* d_save_invstd,
+/* Training-mode BatchNorm2d with an optional fused ReLU and an optional fused
+ * bias of the preceding convolution, for the policy/value CNN's conv stack
+ * (network.py:75-117 conv -> BatchNorm2d -> ReLU, ResidualBlock
+ * network.py:14-30).  Input x is the convolution output WITHOUT its bias;
+ * d_pre_bias (NULL = none) is that bias, added per channel before the
+ * statistics, so the result equals nn.BatchNorm2d(conv(x) + bias).
+ * dtype 0 = f32, 1 = bf16 activations; nhwc 0 = NCHW contiguous (HW * element
+ * size a multiple of 16 bytes), 1 = NHWC / channels_last contiguous (C *
+ * element size = 16 bytes times a power of two <= 256); weight / bias /
+ * statistics are f32.  Forward = nn.BatchNorm2d training forward (batch mean,
+ * biased variance for the normalisation; running_mean / running_var updated
+ * with `momentum` and the unbiased variance when non-NULL), then max(y, 0) if
+ * relu.  d_ws is caller scratch of bb_bn_workspace_bytes(...) bytes (8-byte
+ * aligned).  Backward takes the forward's input x and saved mean / inverse
+ * std; with relu it recomputes the mask from x.  It writes dx and, where
+ * non-NULL, dweight, dbias and d_dpre_bias = sum of dx per channel.  No
+ * atomics: results are deterministic. */
+int64_t bb_bn_workspace_bytes(int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW);
+int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW,
+                  const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps,
+                  int32_t relu, double* d_ws, float* d_save_mean, float* d_save_invstd,
                   float* d_running_mean, float* d_running_var, float momentum,
                   void* d_y, void* stream);
-int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t N,
-                   int32_t C, int32_t HW, const float* d_weight, const float* d_bias,
-                   const float* d_save_mean, const float* d_save_invstd, int32_t relu,
-                   double* d_ws, void* d_dx, float* d_dweight, float* d_dbias,
-                   void* stream);
+int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N,
+                   int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
+                   const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
+                   int32_t relu, double* d_ws, void* d_dx, float* d_dweight, float* d_dbias,
+                   float* d_dpre_bias, void* stream);
 
 #ifdef __cplusplus
 }

@@ -110,16 +110,22 @@ def test_gather_obs_expansion(cuda):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("relu", [False, True])
-@pytest.mark.parametrize("n,c", [(2048, 128), (300, 64), (7, 4)])
-def test_fused_batchnorm_matches_torch(cuda, dtype, relu, n, c):
+@pytest.mark.parametrize("n,c,nhwc", [(2048, 128, False), (300, 64, False), (7, 4, False),
+                                      (2048, 128, True), (300, 64, True), (5, 8, True)])
+def test_fused_batchnorm_matches_torch(cuda, dtype, relu, n, c, nhwc):
     """models.network.BatchNorm2d (HIP bb_bn_forward/backward) vs
     nn.BatchNorm2d [+ ReLU] in training mode: output, running statistics,
     num_batches_tracked, dx / dweight / dbias.  fp32 within 1e-4 (reduction
-    order), bf16 within bf16 rounding of the output."""
+    order), bf16 within bf16 rounding of the output.  NCHW and channels_last
+    (NHWC) layouts; the output keeps the input's layout."""
     from models.network import BatchNorm2d
+    from runtime.kernels import bn_fusable
 
     torch.manual_seed(n + c)
-    x0 = (torch.randn(n, c, 8, 8, device=cuda) * 1.7 + 0.3).to(dtype)
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    x0 = (torch.randn(n, c, 8, 8, device=cuda) * 1.7 + 0.3).to(dtype).contiguous(memory_format=fmt)
+    if nhwc and c * x0.element_size() % 16 == 0:
+        assert bn_fusable(x0)
     ref = torch.nn.BatchNorm2d(c).to(cuda)
     fus = BatchNorm2d(c, relu=relu).to(cuda)
     with torch.no_grad():
@@ -127,10 +133,12 @@ def test_fused_batchnorm_matches_torch(cuda, dtype, relu, n, c):
         for m in (ref, fus):
             m.weight.copy_(w)
             m.bias.copy_(b)
-    g = torch.randn(n, c, 8, 8, device=cuda).to(dtype)
+    g = torch.randn(n, c, 8, 8, device=cuda).to(dtype).contiguous(memory_format=fmt)
     # fused path
     xf = x0.clone().requires_grad_(True)
     yf = fus(xf)
+    if nhwc and bn_fusable(x0):
+        assert yf.is_contiguous(memory_format=torch.channels_last)
     yf.backward(g)
     # reference (fp32 on the same values); with the ReLU, its backward takes the
     # fused forward's own mask (ties at the kink may round either way)
@@ -154,3 +162,53 @@ def test_fused_batchnorm_matches_torch(cuda, dtype, relu, n, c):
     xe = x0.float()[:5]
     ye = fus(xe)
     assert torch.allclose(torch.relu(ref(xe)) if relu else ref(xe), ye, atol=1e-5)
+
+
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_network_fused_conv_bias_batchnorm_matches_torch(cuda, channels_last):
+    """BlockBlastNetwork in training mode with the HIP BatchNorm (conv bias
+    folded into it, NCHW or channels_last) vs the same weights on torch's own
+    conv(+bias) -> nn.BatchNorm2d -> ReLU (use_fused off), fp32: logits,
+    values, every parameter gradient and the BN running statistics.  The conv
+    biases feed a BatchNorm, so their true gradient is 0: both sides must be
+    at rounding level against the weight gradients."""
+    from models.network import BatchNorm2d, BlockBlastNetwork
+
+    torch.manual_seed(11)
+    net = BlockBlastNetwork().to(cuda).train()
+    ref = BlockBlastNetwork().to(cuda).train()
+    ref.load_state_dict(net.state_dict())
+    for n in (net, ref):
+        for m in n.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+    if channels_last:
+        net.to(memory_format=torch.channels_last)
+    x = (torch.rand((512, 4, 8, 8), device=cuda) < 0.4).float()
+    xin = x.contiguous(memory_format=torch.channels_last) if channels_last else x
+    BatchNorm2d.use_fused = True
+    lf, vf = net.raw(xin)
+    BatchNorm2d.use_fused = False
+    try:
+        lr_, vr = ref.raw(x)
+    finally:
+        BatchNorm2d.use_fused = True
+    assert torch.allclose(lf, lr_, rtol=1e-4, atol=1e-4 * float(lr_.detach().abs().max()))
+    assert torch.allclose(vf, vr, rtol=1e-4, atol=1e-4 * float(vr.detach().abs().max()))
+    w = torch.randn_like(lr_)
+    ((lf * w).sum() + vf.sum()).backward()
+    ((lr_ * w).sum() + vr.sum()).backward()
+    named_ref = dict(ref.named_parameters())
+    for name, p in net.named_parameters():
+        g, gr = p.grad, named_ref[name].grad
+        if name.endswith(".bias") and named_ref[name[:-5] + ".weight"].dim() == 4:  # a conv bias
+            wscale = float(named_ref[name.replace(".bias", ".weight")].grad.abs().max())
+            assert float(g.abs().max()) <= 1e-3 * wscale and float(gr.abs().max()) <= 1e-3 * wscale, name
+            continue
+        # relative L2 error: single elements of these long reductions (sum over
+        # batch x 64 positions) differ more between conv algorithms (MIOpen picks
+        # winograd or implicit GEMM per layout) than the norm
+        rel = float((g - gr).norm() / gr.norm().clamp_min(1e-30))
+        assert rel < 5e-3, (name, rel)
+    for (name, b), br in zip(net.named_buffers(), ref.buffers()):
+        assert torch.allclose(b.float(), br.float(), rtol=1e-4, atol=1e-5), name

@@ -134,10 +134,11 @@ def _ddp_worker(rank, world, port, q):
     loss.backward()
     dist.all_reduce(flat)
     flat.div_(world)
+    reduced = torch.cat([p.grad.reshape(-1) for p in agent.network.parameters()])
     mean, std = _global_moments(torch.arange(4, dtype=torch.float32) + 4 * rank)
     gathered = [torch.zeros_like(local) for _ in range(world)]
     dist.all_gather(gathered, local)
-    q.put((rank, torch.allclose(flat, torch.stack(gathered).mean(0), atol=1e-6), float(mean), float(std),
+    q.put((rank, torch.allclose(reduced, torch.stack(gathered).mean(0), atol=1e-6), float(mean), float(std),
            float(sum(p.sum() for p in agent.network.state_dict().values() if p.dtype.is_floating_point))))
     dist.destroy_process_group()
 
