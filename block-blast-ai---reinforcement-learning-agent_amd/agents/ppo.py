@@ -225,10 +225,14 @@ class PPOAgent(BaseAgent):
         self.config = config or PPOConfig()
         self.network = BlockBlastNetwork(conv_channels=self.config.conv_channels,
                                          fc_hidden=self.config.fc_hidden).to(self.device)
-        # capturable: Adam's step count lives on the device, so the whole optimizer
-        # step can be replayed from a HIP graph (see train_minibatch)
+        # On the GPU: capturable (the step count lives on the device, so the
+        # whole optimizer step can be replayed from a HIP graph, see
+        # train_minibatch) and fused (one multi-tensor kernel; the capturable
+        # foreach path divides every tensor by a 0-dim bias correction in a
+        # separate strided kernel, 86 launches per step)
+        on_gpu = self.device.type == "cuda"
         self.optimizer = torch.optim.Adam(self.network.parameters(), lr=self.config.learning_rate, eps=1e-5,
-                                          capturable=self.device.type == "cuda")
+                                          capturable=on_gpu, fused=True if on_gpu else None)
         self.scheduler = None
         # Philox key for rollout sampling (derived from torch's seeded RNG)
         self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if sample_seed is None else int(sample_seed)
@@ -456,9 +460,9 @@ class PPOAgent(BaseAgent):
     # ----------------------------------------------------------- checkpoint
     def save(self, path: str) -> None:
         """ppo.py:425-431 (same dict keys).  Saved as a plain Adam (capturable
-        off), so the reference's own Adam loads it on any device."""
+        and fused off), so the reference's own Adam loads it on any device."""
         opt = self.optimizer.state_dict()
-        opt["param_groups"] = [dict(g, capturable=False) for g in opt["param_groups"]]
+        opt["param_groups"] = [dict(g, capturable=False, fused=None) for g in opt["param_groups"]]
         torch.save({"network_state_dict": self.network.state_dict(),
                     "optimizer_state_dict": opt,
                     "config": self.config.to_dict()}, path)
@@ -472,6 +476,7 @@ class PPOAgent(BaseAgent):
             cap = self.device.type == "cuda"
             for g in self.optimizer.param_groups:
                 g["capturable"] = cap
+                g["fused"] = True if cap else None
             for st in self.optimizer.state.values():  # capturable Adam keeps its step count on the device
                 if "step" in st and torch.is_tensor(st["step"]):
                     st["step"] = st["step"].to(self.device if cap else "cpu", torch.float32)

@@ -34,7 +34,7 @@ def summarize(path, steps):
     print(f"marker found: {bool(marks)}; window {span/1e6:.2f} ms over {steps} steps = {span/1e3/steps:.1f} us/step; "
           f"kernel busy {100*busy/span:.1f}%; {len(sel)/steps:.1f} kernels/step")
     for k, (d, c) in sorted(acc.items(), key=lambda kv: -kv[1][0])[:40]:
-        print(f"{100*d/busy:6.2f}% {c/steps:6.1f}/step {d/c/1e3:8.1f}us {d/1e3/steps:8.1f}us/step  {k[:110]}")
+        print(f"{100*d/busy:6.2f}% {c/steps:6.1f}/step {d/c/1e3:8.1f}us {d/1e3/steps:8.1f}us/step  {k[:230]}")
 
 
 def main():
