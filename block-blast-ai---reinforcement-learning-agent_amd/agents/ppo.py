@@ -231,6 +231,12 @@ class PPOAgent(BaseAgent):
         # foreach path divides every tensor by a 0-dim bias correction in a
         # separate strided kernel, 86 launches per step)
         on_gpu = self.device.type == "cuda"
+        # conv-stack activations NHWC on the GPU (set_channels_last): no NCHW<->NHWC
+        # transposes around MIOpen's implicit-GEMM convolutions
+        self.channels_last = False
+        if on_gpu:
+            self.network.to(memory_format=torch.channels_last)
+            self.channels_last = True
         self.optimizer = torch.optim.Adam(self.network.parameters(), lr=self.config.learning_rate, eps=1e-5,
                                           capturable=on_gpu, fused=True if on_gpu else None)
         self.scheduler = None
@@ -242,7 +248,6 @@ class PPOAgent(BaseAgent):
         # one optimizer step per minibatch replayed from a HIP graph (CUDA device, one process)
         self.use_graphs = self.device.type == "cuda"
         self._graphs = {}
-        self.channels_last = False
 
     # ------------------------------------------------------------ helpers
     def set_channels_last(self, on: bool = True) -> None:

@@ -528,6 +528,7 @@ extern "C" int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32
   if (rc != BB_OK) return rc;
   if (!d_x || !d_weight || !d_bias || !d_ws || !d_save_mean || !d_save_invstd || !d_y)
     return fail(nullptr, BB_ERR_ARG, "bb_bn_forward: NULL argument");
+  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
   hipError_t st = launch_bn_forward(d_x, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
                                     d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum, d_y,
                                     (hipStream_t)stream);
@@ -543,6 +544,7 @@ extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, 
   if (rc != BB_OK) return rc;
   if (!d_x || !d_dy || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx)
     return fail(nullptr, BB_ERR_ARG, "bb_bn_backward: NULL argument");
+  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
   hipError_t st = launch_bn_backward(d_x, d_dy, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, d_save_mean,
                                      d_save_invstd, relu, d_ws, d_dx, d_dweight, d_dbias, d_dpre_bias,
                                      (hipStream_t)stream);

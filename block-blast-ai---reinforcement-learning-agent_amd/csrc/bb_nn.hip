@@ -224,21 +224,54 @@ __global__ void __launch_bounds__(kBnThreads) bn_sum_partials(const double* __re
     for (int m = 0; m < kQ; ++m) sums[c * kQ + m] = a[m];
 }
 
-// Per-channel finalisation (one thread per channel): mean, inverse std of the
+// Per-channel coefficients of the elementwise passes, packed 8 floats per
+// channel so an apply thread loads them as two 16-byte vectors:
+//   forward  {pre_bias, mean, invstd * weight, bias, -, -, -, -}
+//   backward {pre_bias, mean, invstd * weight, bias, invstd, mean(g), mean(g * xhat), -}
+constexpr int kCoef = 8;
+
+// Forward finalisation (one thread per channel): mean, inverse std of the
 // biased variance (the normalisation), running statistics with the unbiased
-// variance (nn.BatchNorm2d, momentum = exponential_average_factor).
+// variance (nn.BatchNorm2d, momentum = exponential_average_factor), coefficients.
 __global__ void bn_finalize_fwd(int C, double M, const double* __restrict__ sums, float eps,
-                                float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                float* __restrict__ rmean, float* __restrict__ rvar, float momentum) {
+                                const float* __restrict__ pre_bias, const float* __restrict__ w,
+                                const float* __restrict__ b, float* __restrict__ save_mean,
+                                float* __restrict__ save_invstd, float* __restrict__ rmean, float* __restrict__ rvar,
+                                float momentum, float* __restrict__ coef) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double m = sums[kQ * c] / M;
   double var = sums[kQ * c + 1] / M - m * m;
   if (var < 0.0) var = 0.0;
-  save_mean[c] = (float)m;
-  save_invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)m;
+  const float mu = (float)m, is = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = mu;
+  save_invstd[c] = is;
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
   if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1.0 ? var * M / (M - 1.0) : var);
+  float4* o = reinterpret_cast<float4*>(coef + kCoef * c);
+  o[0] = make_float4(pre_bias ? pre_bias[c] : 0.f, mu, is * w[c], b[c]);
+}
+
+// Backward finalisation (one thread per channel): dweight = sum(g * xhat),
+// dbias = sum(g), the convolution bias gradient sum(dx) (dx = sc * (g - mg -
+// xhat * mgx) summed in fp64), coefficients.
+__global__ void bn_finalize_bwd(int C, double M, const double* __restrict__ sums, const float* __restrict__ pre_bias,
+                                const float* __restrict__ w, const float* __restrict__ b,
+                                const float* __restrict__ mean, const float* __restrict__ invstd,
+                                float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dpb,
+                                float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invM = (float)(1.0 / M);
+  const double sg = sums[kQ * c], sgx = sums[kQ * c + 1], sx = sums[kQ * c + 2];
+  const float is = invstd[c], sc = is * w[c];
+  const float mg = (float)sg * invM, mgx = (float)sgx * invM;
+  if (dw) dw[c] = (float)sgx;
+  if (db) db[c] = (float)sg;
+  if (dpb) dpb[c] = (float)((double)sc * (sg - M * (double)mg) - (double)sc * (double)mgx * sx);
+  float4* o = reinterpret_cast<float4*>(coef + kCoef * c);
+  o[0] = make_float4(pre_bias ? pre_bias[c] : 0.f, mean[c], sc, b[c]);
+  o[1] = make_float4(is, mg, mgx, 0.f);
 }
 
 // Channel of element j of 16-byte chunk i: NCHW rows are (n, c) with HW / V
@@ -247,33 +280,26 @@ __global__ void bn_finalize_fwd(int C, double M, const double* __restrict__ sums
 // a thread's channels are fixed and their coefficients stay in registers.
 template <typename T, bool NHWC>
 __global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restrict__ x, void* __restrict__ y,
-                                                           int64_t total, int C, int cpr,
-                                                           const float* __restrict__ pre_bias,
-                                                           const float* __restrict__ w, const float* __restrict__ b,
-                                                           int relu, const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd) {
+                                                           int64_t total, int C, int cpr, int relu,
+                                                           const float* __restrict__ coef) {
   constexpr int V = Vec<T>::N;
   constexpr int NC = NHWC ? V : 1;
+  const float4* cf = reinterpret_cast<const float4*>(coef);
   const int64_t g0 = (int64_t)blockIdx.x * kBnThreads + threadIdx.x;
-  float pb[NC], mu[NC], sc[NC], sh[NC];
-  auto load_coef = [&](int c0) {
+  float4 k[NC];
+  if (NHWC) {
+    const int c0 = (int)(g0 % cpr) * V;
 #pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      pb[j] = pre_bias ? pre_bias[c0 + j] : 0.f;
-      mu[j] = mean[c0 + j];
-      sc[j] = invstd[c0 + j] * w[c0 + j];
-      sh[j] = b[c0 + j];
-    }
-  };
-  if (NHWC) load_coef((int)(g0 % cpr) * V);
+    for (int j = 0; j < NC; ++j) k[j] = cf[(c0 + j) * (kCoef / 4)];
+  }
   for (int64_t i = g0; i < total; i += (int64_t)gridDim.x * kBnThreads) {
-    if (!NHWC) load_coef((int)((i / cpr) % C));
+    if (!NHWC) k[0] = cf[(int)((i / cpr) % C) * (kCoef / 4)];
     float f[V];
     Vec<T>::load(x, i, f);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const int jc = NHWC ? j : 0;
-      const float v = (f[j] + pb[jc] - mu[jc]) * sc[jc] + sh[jc];
+      const float4& q = k[NHWC ? j : 0];  // {pb, mu, sc, sh}
+      const float v = (f[j] + q.x - q.y) * q.z + q.w;
       f[j] = relu ? fmaxf(v, 0.f) : v;
     }
     Vec<T>::store(y, i, f);
@@ -283,54 +309,37 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restric
 template <typename T, bool NHWC>
 __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restrict__ x, const void* __restrict__ dy,
                                                            void* __restrict__ dx, int64_t total, int C, int cpr,
-                                                           double M, const float* __restrict__ pre_bias,
-                                                           const float* __restrict__ w, const float* __restrict__ b,
-                                                           const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd, int relu,
-                                                           const double* __restrict__ sums, float* __restrict__ dw,
-                                                           float* __restrict__ db, float* __restrict__ dpb) {
+                                                           int relu, const float* __restrict__ coef) {
   constexpr int V = Vec<T>::N;
   constexpr int NC = NHWC ? V : 1;
-  const float invM = (float)(1.0 / M);
+  const float4* cf = reinterpret_cast<const float4*>(coef);
   const int64_t g0 = (int64_t)blockIdx.x * kBnThreads + threadIdx.x;
-  if (g0 < C) {
-    const int c = (int)g0;
-    const double sg = sums[kQ * c], sgx = sums[kQ * c + 1], sx = sums[kQ * c + 2];
-    if (dw) dw[c] = (float)sgx;
-    if (db) db[c] = (float)sg;
-    if (dpb) {  // sum over positions of dx = sc * (g - mg - xhat * mgx), evaluated in fp64
-      const double sc = (double)(invstd[c] * w[c]);
-      const double mg = (double)((float)sg * invM), mgx = (double)((float)sgx * invM);
-      dpb[c] = (float)(sc * (sg - M * mg) - sc * mgx * sx);
-    }
-  }
-  float pb[NC], mu[NC], is[NC], sc[NC], sh[NC], mg[NC], mgx[NC];
-  auto load_coef = [&](int c0) {
+  float4 k0[NC], k1[NC];
+  if (NHWC) {
+    const int c0 = (int)(g0 % cpr) * V;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      const int c = c0 + j;
-      pb[j] = pre_bias ? pre_bias[c] : 0.f;
-      mu[j] = mean[c];
-      is[j] = invstd[c];
-      sc[j] = is[j] * w[c];
-      sh[j] = b[c];
-      mg[j] = (float)sums[kQ * c] * invM;
-      mgx[j] = (float)sums[kQ * c + 1] * invM;
+      k0[j] = cf[(c0 + j) * (kCoef / 4)];
+      k1[j] = cf[(c0 + j) * (kCoef / 4) + 1];
     }
-  };
-  if (NHWC) load_coef((int)(g0 % cpr) * V);
+  }
   for (int64_t i = g0; i < total; i += (int64_t)gridDim.x * kBnThreads) {
-    if (!NHWC) load_coef((int)((i / cpr) % C));
+    if (!NHWC) {
+      const int c = (int)((i / cpr) % C);
+      k0[0] = cf[c * (kCoef / 4)];
+      k1[0] = cf[c * (kCoef / 4) + 1];
+    }
     float fx[V], fg[V];
     Vec<T>::load(x, i, fx);
     Vec<T>::load(dy, i, fg);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const int jc = NHWC ? j : 0;
-      const float u = fx[j] + pb[jc];
-      const float g = (relu && (u - mu[jc]) * sc[jc] + sh[jc] <= 0.f) ? 0.f : fg[j];
-      const float xh = (u - mu[jc]) * is[jc];
-      fx[j] = sc[jc] * (g - mg[jc] - xh * mgx[jc]);
+      const float4& a = k0[NHWC ? j : 0];  // {pb, mu, sc, sh}
+      const float4& q = k1[NHWC ? j : 0];  // {is, mg, mgx, -}
+      const float u = fx[j] + a.x;
+      const float g = (relu && (u - a.y) * a.z + a.w <= 0.f) ? 0.f : fg[j];  // the forward's exact ops
+      const float xh = (u - a.y) * q.x;
+      fx[j] = a.z * (g - q.y - xh * q.z);
     }
     Vec<T>::store(dx, i, fx);
   }
@@ -352,7 +361,7 @@ Plan plan_for(int esz, int nhwc, int N, int C, int HW) {
     const int rows_per_iter = kBnThreads / p.cpr;
     const int64_t R = (int64_t)N * HW;
     int64_t g = (R + (int64_t)rows_per_iter * kUnroll * 2 - 1) / ((int64_t)rows_per_iter * kUnroll * 2);
-    p.nb = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));  // >= 2 unrolled passes per thread
+    p.nb = (int)(g < 1 ? 1 : (g > 256 ? 256 : g));  // >= 2 unrolled passes per thread
     p.rgrid = dim3(p.nb);
   } else {
     p.cpr = HW / p.V;
@@ -391,23 +400,35 @@ void launch_reduce(const Plan& p, int nhwc, const void* x, const void* dy, int N
   hipLaunchKernelGGL(bn_sum_partials, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, part, p.nb, C, sums);
 }
 
+// Workspace (16-byte aligned): coefficients [C][kCoef] floats (float4 loads),
+// sums [C][kQ] doubles, partials [nb][C][kQ] doubles.
+struct Ws {
+  float* coef;
+  double* sums;
+  double* part;
+};
+Ws split_ws(double* ws, int C) {
+  Ws w;
+  w.coef = reinterpret_cast<float*>(ws);
+  w.sums = ws + kCoef / 2 * C;
+  w.part = w.sums + kQ * C;
+  return w;
+}
+
 template <typename T>
 hipError_t bn_forward_t(const void* x, int nhwc, int N, int C, int HW, const float* pb, const float* w,
                         const float* b, float eps, int relu, double* ws, float* save_mean, float* save_invstd,
                         float* rmean, float* rvar, float momentum, void* y, hipStream_t s) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
-  double* sums = ws;
-  double* part = ws + kQ * C;
-  launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, part, sums, s);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 255) / 256), dim3(256), 0, s, C, (double)N * HW, sums, eps, save_mean,
-                     save_invstd, rmean, rvar, momentum);
+  const Ws k = split_ws(ws, C);
+  launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, k.part, k.sums, s);
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 255) / 256), dim3(256), 0, s, C, (double)N * HW, k.sums, eps, pb, w,
+                     b, save_mean, save_invstd, rmean, rvar, momentum, k.coef);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
-    hipLaunchKernelGGL((bn_apply_fwd<T, true>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, pb, w, b, relu,
-                       save_mean, save_invstd);
+    hipLaunchKernelGGL((bn_apply_fwd<T, true>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, relu, k.coef);
   else
-    hipLaunchKernelGGL((bn_apply_fwd<T, false>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, pb, w, b,
-                       relu, save_mean, save_invstd);
+    hipLaunchKernelGGL((bn_apply_fwd<T, false>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, relu, k.coef);
   return hipGetLastError();
 }
 
@@ -416,17 +437,17 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
                          const float* w, const float* b, const float* mean, const float* invstd, int relu, double* ws,
                          void* dx, float* dw, float* db, float* dpb, hipStream_t s) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
-  double* sums = ws;
-  double* part = ws + kQ * C;
-  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, part, sums, s);
-  const dim3 ge(grid_for_elems(p.chunks > C ? p.chunks : C, nhwc));
-  const double M = (double)N * HW;
+  const Ws k = split_ws(ws, C);
+  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, k.sums, s);
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 255) / 256), dim3(256), 0, s, C, (double)N * HW, k.sums, pb, w, b,
+                     mean, invstd, dw, db, dpb, k.coef);
+  const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
-    hipLaunchKernelGGL((bn_apply_bwd<T, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, M, pb, w,
-                       b, mean, invstd, relu, sums, dw, db, dpb);
+    hipLaunchKernelGGL((bn_apply_bwd<T, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
+                       k.coef);
   else
-    hipLaunchKernelGGL((bn_apply_bwd<T, false>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, M, pb, w,
-                       b, mean, invstd, relu, sums, dw, db, dpb);
+    hipLaunchKernelGGL((bn_apply_bwd<T, false>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
+                       k.coef);
   return hipGetLastError();
 }
 
@@ -434,7 +455,7 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
 
 int64_t bn_workspace_bytes(int dtype, int nhwc, int N, int C, int HW) {
   const Plan p = plan_for(dtype == 1 ? 2 : 4, nhwc, N, C, HW);
-  return (int64_t)sizeof(double) * kQ * C * (1 + (int64_t)p.nb);
+  return (int64_t)sizeof(double) * C * (kQ + kCoef / 2 + kQ * (int64_t)p.nb);
 }
 
 hipError_t launch_bn_forward(const void* x, int dtype, int nhwc, int N, int C, int HW, const float* pb,

@@ -251,7 +251,7 @@ int bb_gather_obs(const uint64_t* d_board, const uint32_t* d_hand,
  * statistics are f32.  Forward = nn.BatchNorm2d training forward (batch mean,
  * biased variance for the normalisation; running_mean / running_var updated
  * with `momentum` and the unbiased variance when non-NULL), then max(y, 0) if
- * relu.  d_ws is caller scratch of bb_bn_workspace_bytes(...) bytes (8-byte
+ * relu.  d_ws is caller scratch of bb_bn_workspace_bytes(...) bytes (16-byte
  * aligned).  Backward takes the forward's input x and saved mean / inverse
  * std; with relu it recomputes the mask from x.  It writes dx and, where
  * non-NULL, dweight, dbias and d_dpre_bias = sum of dx per channel.  No

@@ -40,11 +40,11 @@ def test_reference_api_rollout_and_update(cuda):
                 np.logical_or(term, trunc).astype(np.float32), values)
         obs = nobs
     assert buf.full
-    w0 = torch.nn.utils.parameters_to_vector(agent.network.parameters()).detach().clone()
+    w0 = torch.cat([p.reshape(-1) for p in agent.network.parameters()]).detach().clone()
     m = agent.update(buf, agent.get_values(obs))
     assert set(m) == {"policy_loss", "value_loss", "entropy", "total_loss", "approx_kl", "clip_fraction"}
     assert all(np.isfinite(v) for v in m.values())
-    w1 = torch.nn.utils.parameters_to_vector(agent.network.parameters()).detach()
+    w1 = torch.cat([p.reshape(-1) for p in agent.network.parameters()]).detach()
     assert not torch.equal(w0, w1)
     env.close()
 
@@ -159,12 +159,14 @@ def test_graphed_minibatch_step_matches_eager(cuda, autocast):
     eager, graphed = make(), make()
     eager.use_graphs = False
     assert graphed.use_graphs
-    # fp32: the two paths agree to rounding; bf16: the first step agrees to bf16
-    # rounding, later ones drift apart (different accumulation orders compound)
+    # the first step agrees to rounding (fp32) / bf16 rounding; later ones drift
+    # apart a little: MIOpen's split-K weight-gradient convolutions accumulate
+    # with atomics, so even two eager runs differ in the last bits, and Adam
+    # compounds it
     for k, b in enumerate(batches):
         s_e = eager.train_minibatch(*b).clone()
         s_g = graphed.train_minibatch(*b).clone()
-        tol = 1e-4 if autocast is None else (2e-2 if k == 0 else 1.5e-1)
+        tol = (1e-4 if k == 0 else 2e-3) if autocast is None else (2e-2 if k == 0 else 1.5e-1)
         assert torch.allclose(s_e, s_g, rtol=tol, atol=tol), (k, s_e, s_g)
     assert len(graphed._graphs) == 1
     if autocast is None:  # Adam moves near-zero gradients by ~lr either way: weights agree to a few lr

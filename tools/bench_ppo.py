@@ -32,7 +32,8 @@ def main():
     ap.add_argument("--update-steps", type=int, default=100)
     ap.add_argument("--autocast", choices=["none", "bf16"], default="none")
     ap.add_argument("--miopen-find", action="store_true", help="torch.backends.cudnn.benchmark = True")
-    ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--layout", choices=["default", "nchw", "channels_last"], default="default",
+                    help="conv-stack activation layout (default: the agent's own choice)")
     ap.add_argument("--no-graph", action="store_true", help="issue the update step kernel by kernel")
     args = ap.parse_args()
 
@@ -46,8 +47,8 @@ def main():
     agent = PPOAgent(PPOConfig(batch_size=args.batch, num_epochs=args.epochs), device=dev, sample_seed=1)
     if args.autocast == "bf16":
         agent.autocast_dtype = torch.bfloat16
-    if args.channels_last:
-        agent.network.to(memory_format=torch.channels_last)
+    if args.layout != "default":
+        agent.set_channels_last(args.layout == "channels_last")
     agent.use_graphs = not args.no_graph
     agent.train()
     roll = DeviceRollout(args.envs, 0, args.envs, 42, {}, args.rollout, dev)
@@ -89,7 +90,7 @@ def main():
     upd_flops = 3 * FWD_FLOP * args.batch / t_upd_step
     print(json.dumps({
         "workload": "BASELINE config 3: full PPO iteration on 1 MI355X", "envs": args.envs, "rollout_steps": args.rollout,
-        "miopen_find": args.miopen_find, "channels_last": args.channels_last,
+        "miopen_find": args.miopen_find, "channels_last": agent.channels_last,
         "batch": args.batch, "epochs": args.epochs, "compute_dtype": "bf16 autocast" if args.autocast == "bf16" else "fp32",
         "rollout_s": round(t_roll, 4), "rollout_env_steps_per_s": round(samples / t_roll, 1),
         "rollout_cnn_tflops": round(roll_flops / 1e12, 2),
