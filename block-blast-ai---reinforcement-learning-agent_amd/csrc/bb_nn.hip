@@ -31,7 +31,9 @@ namespace bb {
 namespace {
 
 constexpr int kBnThreads = 256;
-constexpr int kUnroll = 4;  // rows in flight per thread in the NHWC reductions
+// rows in flight per thread in the NHWC reductions (forward: one tensor; backward: x and dy)
+template <bool BWD>
+constexpr int kUnroll = BWD ? 4 : 8;
 constexpr int kQ = 3;       // partial quantities per channel
 
 template <typename T>
@@ -177,10 +179,10 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
     s[j] = q[j] = t[j] = 0.f;
   }
   const int stride = gridDim.x * rows_per_iter;
-  for (int n0 = blockIdx.x * rows_per_iter + r; n0 < R; n0 += kUnroll * stride) {
-    float fx[kUnroll][V], fg[kUnroll][BWD ? V : 1];
+  for (int n0 = blockIdx.x * rows_per_iter + r; n0 < R; n0 += kUnroll<BWD> * stride) {
+    float fx[kUnroll<BWD>][V], fg[kUnroll<BWD>][BWD ? V : 1];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {  // all loads in flight before the arithmetic
+    for (int u = 0; u < kUnroll<BWD>; ++u) {  // all loads in flight before the arithmetic
       const int n = n0 + u * stride;
       if (n < R) {
         Vec<T>::load(x, (int64_t)n * cpr + kc, fx[u]);
@@ -188,7 +190,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
       }
     }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < kUnroll<BWD>; ++u) {
       if (n0 + u * stride >= R) break;
 #pragma unroll
       for (int j = 0; j < V; ++j) accumulate<BWD>(fx[u][j], BWD ? fg[u][j] : 0.f, k[j], relu, s[j], q[j], t[j]);
@@ -360,8 +362,8 @@ Plan plan_for(int esz, int nhwc, int N, int C, int HW) {
     p.cpr = C / p.V;
     const int rows_per_iter = kBnThreads / p.cpr;
     const int64_t R = (int64_t)N * HW;
-    int64_t g = (R + (int64_t)rows_per_iter * kUnroll * 2 - 1) / ((int64_t)rows_per_iter * kUnroll * 2);
-    p.nb = (int)(g < 1 ? 1 : (g > 256 ? 256 : g));  // >= 2 unrolled passes per thread
+    int64_t g = (R + (int64_t)rows_per_iter * 8 - 1) / ((int64_t)rows_per_iter * 8);
+    p.nb = (int)(g < 1 ? 1 : (g > 512 ? 512 : g));  // >= 8 rows per thread
     p.rgrid = dim3(p.nb);
   } else {
     p.cpr = HW / p.V;
