@@ -214,6 +214,27 @@ def categorical_log_prob(probs: torch.Tensor, action: torch.Tensor) -> torch.Ten
     return torch.log(p.clamp(min=_EPS32, max=1.0 - _EPS32)).gather(-1, action.unsqueeze(-1)).squeeze(-1)
 
 
+def ppo_loss_torch(logits, values, masks, actions, old_log_probs, advantages, returns, cfg: "PPOConfig"):
+    """ppo.py:362-392 on torch ops: the CPU path and the parity reference of
+    the fused bb_ppo_loss kernels.  Returns (loss, 6 detached statistics)."""
+    masked = logits + torch.where(masks.bool(), torch.zeros_like(logits), torch.full_like(logits, float("-inf")))
+    probs = F.softmax(masked, dim=-1)
+    new_log_probs = categorical_log_prob(probs, actions)
+    entropy = masked_entropy(probs, masks)
+    ratio = torch.exp(new_log_probs - old_log_probs)
+    surr1 = ratio * advantages
+    surr2 = torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon) * advantages
+    policy_loss = -torch.min(surr1, surr2).mean()
+    value_loss = F.mse_loss(values, returns)
+    entropy_loss = -entropy.mean()
+    loss = policy_loss + cfg.value_coef * value_loss + cfg.entropy_coef * entropy_loss
+    with torch.no_grad():
+        approx_kl = ((ratio - 1) - torch.log(ratio)).mean()
+        clip_fraction = ((ratio - 1).abs() > cfg.clip_epsilon).float().mean()
+        stats = torch.stack([policy_loss, value_loss, entropy.mean(), loss, approx_kl, clip_fraction]).detach()
+    return loss, stats
+
+
 class PPOAgent(BaseAgent):
     """ppo.py:221-449."""
 
@@ -248,6 +269,7 @@ class PPOAgent(BaseAgent):
         # one optimizer step per minibatch replayed from a HIP graph (CUDA device, one process)
         self.use_graphs = self.device.type == "cuda"
         self._graphs = {}
+        self.fused_loss = True  # the minibatch loss on bb_ppo_loss_* (GPU tensors only)
 
     # ------------------------------------------------------------ helpers
     def set_channels_last(self, on: bool = True) -> None:
@@ -344,22 +366,10 @@ class PPOAgent(BaseAgent):
     def _minibatch_loss(self, x, masks, actions, old_log_probs, advantages, returns):
         cfg = self.config
         logits, values = self._raw(x)
-        masked = logits + torch.where(masks.bool(), torch.zeros_like(logits), torch.full_like(logits, float("-inf")))
-        probs = F.softmax(masked, dim=-1)
-        new_log_probs = categorical_log_prob(probs, actions)
-        entropy = masked_entropy(probs, masks)
-        ratio = torch.exp(new_log_probs - old_log_probs)
-        surr1 = ratio * advantages
-        surr2 = torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon) * advantages
-        policy_loss = -torch.min(surr1, surr2).mean()
-        value_loss = F.mse_loss(values, returns)
-        entropy_loss = -entropy.mean()
-        loss = policy_loss + cfg.value_coef * value_loss + cfg.entropy_coef * entropy_loss
-        with torch.no_grad():
-            approx_kl = ((ratio - 1) - torch.log(ratio)).mean()
-            clip_fraction = ((ratio - 1).abs() > cfg.clip_epsilon).float().mean()
-            stats = torch.stack([policy_loss, value_loss, entropy.mean(), loss, approx_kl, clip_fraction]).detach()
-        return loss, stats
+        if self.fused_loss and logits.is_cuda:  # bb_ppo_loss_forward/backward
+            return K.PPOLossFunction.apply(logits, values, masks, actions, old_log_probs, advantages, returns,
+                                           cfg.clip_epsilon, cfg.value_coef, cfg.entropy_coef)
+        return ppo_loss_torch(logits, values, masks, actions, old_log_probs, advantages, returns, cfg)
 
     def _optimizer_step(self, loss: torch.Tensor) -> None:
         world = _world()

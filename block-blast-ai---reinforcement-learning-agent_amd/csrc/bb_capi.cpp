@@ -551,3 +551,35 @@ extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, 
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_backward");
   return BB_OK;
 }
+
+extern "C" int64_t bb_ppo_loss_workspace_bytes(int32_t B) {
+  if (B <= 0) return -1;
+  return ppo_loss_workspace_bytes(B);
+}
+
+extern "C" int bb_ppo_loss_forward(const float* d_logits, const float* d_values, const float* d_mask,
+                                   const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                                   const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
+                                   double* d_ws, float* d_stats, float* d_loss, void* stream) {
+  if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret || !d_ws ||
+      !d_stats)
+    return fail(nullptr, BB_ERR_ARG, "bb_ppo_loss_forward: bad arguments");
+  hipError_t st = launch_ppo_loss_forward(d_logits, d_values, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip,
+                                          value_coef, entropy_coef, d_ws, d_stats, d_loss, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_ppo_loss_forward");
+  return BB_OK;
+}
+
+extern "C" int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const float* d_mask,
+                                    const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                                    const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
+                                    const float* d_grad_loss, float* d_dlogits, float* d_dvalues, void* stream) {
+  if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret ||
+      !d_grad_loss || !d_dlogits || !d_dvalues)
+    return fail(nullptr, BB_ERR_ARG, "bb_ppo_loss_backward: bad arguments");
+  hipError_t st = launch_ppo_loss_backward(d_logits, d_values, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip,
+                                           value_coef, entropy_coef, d_grad_loss, d_dlogits, d_dvalues,
+                                           (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_ppo_loss_backward");
+  return BB_OK;
+}

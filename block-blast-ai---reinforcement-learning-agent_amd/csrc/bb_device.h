@@ -203,20 +203,29 @@ __device__ __forceinline__ int select_bit(uint64_t x, uint32_t k) {
   return pos;
 }
 
-// Synthetic random policy: the k-th legal action, k = (u * popcount) >> 32.
-__device__ __forceinline__ int32_t random_policy(uint64_t m0, uint64_t m1, uint64_t m2, uint64_t seed,
-                                                 uint64_t idx, uint64_t step) {
+// Synthetic random policy: the k-th legal action, k = (u * popcount) >> 32,
+// u = word 0 of Philox4x32-10 at counter (idx, step) under key seed.
+__device__ __forceinline__ uint32_t policy_uniform(uint64_t seed, uint64_t idx, uint64_t step) {
   uint32_t w[4];
   philox_words(seed, idx, step, w);
+  return w[0];
+}
+
+__device__ __forceinline__ int32_t random_policy_u(uint64_t m0, uint64_t m1, uint64_t m2, uint32_t u) {
   uint32_t c0 = __popcll(m0), c1 = __popcll(m1), c2 = __popcll(m2);
   uint32_t tot = c0 + c1 + c2;
   if (tot == 0) return 0;
-  uint32_t k = (uint32_t)(((uint64_t)w[0] * tot) >> 32);
+  uint32_t k = (uint32_t)(((uint64_t)u * tot) >> 32);
   if (k < c0) return select_bit(m0, k);
   k -= c0;
   if (k < c1) return 64 + select_bit(m1, k);
   k -= c1;
   return 128 + select_bit(m2, k);
+}
+
+__device__ __forceinline__ int32_t random_policy(uint64_t m0, uint64_t m1, uint64_t m2, uint64_t seed,
+                                                 uint64_t idx, uint64_t step) {
+  return random_policy_u(m0, m1, m2, policy_uniform(seed, idx, step));
 }
 
 }  // namespace bb

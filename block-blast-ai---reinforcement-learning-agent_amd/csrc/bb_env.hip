@@ -658,6 +658,11 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   uint32_t* my_prog = r.prog + simd_key * 16u + wslot;
   const uint32_t* partner_prog = r.prog + simd_key * 16u + (wslot ^ 1u);
   uint32_t partner = 0;
+  // The policy uniforms are shared by an env's copies: on every kCopies-th
+  // step copy c draws the uniform of step + 1 + c, and each step reads its
+  // uniform from the copy that drew it (one Philox per lane per kCopies steps).
+  constexpr int kCopies = 64 / kRollEnvs;
+  uint32_t u_drawn = 0;
 #pragma unroll 1
   for (int step = 0; step < r.steps; ++step) {
 #if BB_ROLL_FAIR == 1
@@ -762,6 +767,9 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     }
 #endif
     BB_DIAG_T(c2);
+    if (step % kCopies == 0)
+      u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + step + 1 + half);
+    const uint32_t u_next = __shfl(u_drawn, (lane % kRollEnvs) + kRollEnvs * (step % kCopies));
     if (live) {
       masks_of(t, s.B, s.hand, m);
       double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
@@ -808,7 +816,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         r.mask[3 * o + 1] = m[1];
         r.mask[3 * o + 2] = m[2];
       }
-      act = random_policy(m[0], m[1], m[2], a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + step + 1);
+      act = random_policy_u(m[0], m[1], m[2], u_next);  // Philox (seed, env, policy_step0 + step + 1)
     }
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
     BB_DIAG_T(c3);

@@ -100,6 +100,15 @@ hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
                               int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s);
 
+int64_t ppo_loss_workspace_bytes(int B);
+hipError_t launch_ppo_loss_forward(const float* logits, const float* values, const float* mask, const int64_t* actions,
+                                   const float* old_logp, const float* adv, const float* ret, int B, float clip,
+                                   float vcoef, float ecoef, double* ws, float* stats, float* loss, hipStream_t s);
+hipError_t launch_ppo_loss_backward(const float* logits, const float* values, const float* mask,
+                                    const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
+                                    int B, float clip, float vcoef, float ecoef, const float* gloss, float* dlogits,
+                                    float* dvalues, hipStream_t s);
+
 // Host helpers (bb_tables.cpp).
 void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces]);
 void build_jump_table(JumpRow rows[kJumpMax + 1]);

@@ -1,0 +1,245 @@
+// bb_loss.hip -- the PPO minibatch loss of PPOAgent.update (ppo.py:362-401)
+// with the masked-categorical tail of BlockBlastNetwork (network.py:173-180,
+// 210-262), forward and backward, fused (gfx950).
+//
+// Issued as torch ops the loss is ~45 elementwise / reduction kernels forward
+// and as many backward, each a few microseconds on 2,048 x 192 logits; here it
+// is one wave per minibatch row for each direction plus a one-wave finaliser.
+//
+// Per row (torch fp32 semantics, same operation order as the torch path):
+//   p      = softmax(logits + where(mask, 0, -inf))
+//   P      = p / sum(p)                         Categorical(probs) normalisation
+//   logp   = log(clamp(P[a], eps, 1 - eps))     Categorical.log_prob (clamp_probs)
+//   ent    = masked entropy of p (network.py:232-262, clamps 1e-10)
+//   ratio  = exp(logp - old_logp)
+//   pol    = -min(ratio * A, clamp(ratio, 1 - c, 1 + c) * A)
+//   vloss  = (value - ret)^2
+// Loss = mean(pol) + vcoef * mean(vloss) - ecoef * mean(ent); the statistics
+// (policy / value / entropy / total loss, approx_kl = mean((r - 1) - log r),
+// clip_fraction = mean(|r - 1| > c)) come from fp64 block partials summed in a
+// fixed order.  Backward follows torch's autograd rules: torch.min splits ties
+// half/half, clamp passes the gradient on its closed interval, log divides by
+// the clamped value.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "bb_env_internal.h"
+
+namespace bb {
+
+namespace {
+
+constexpr int kLossThreads = 256;
+constexpr int kRowsPerBlock = kLossThreads / 64;
+constexpr int kStats = 5;  // partial sums: pol, vloss, ent, kl, clipped
+constexpr float kEps32 = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
+
+__device__ __forceinline__ float wmax(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o));
+  return v;
+}
+
+// The forward quantities of one row, 3 entries per lane (action j * 64 + lane).
+struct RowFwd {
+  bool valid[3];
+  float p[3];     // softmax of the masked logits
+  float s;        // sum of p
+  float pa;       // P[a] = p[a] / s (all lanes)
+  float ms_raw;   // sum of the masked p
+  float ms;       // clamp(ms_raw, 1e-10)
+  float q[3];     // masked p / ms
+  float logp, ent;
+};
+
+__device__ __forceinline__ void row_forward(const float* __restrict__ logits, const float* __restrict__ mask,
+                                            int64_t row, int64_t a, int lane, RowFwd& r) {
+  float x[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    x[j] = logits[row * 192 + j * 64 + lane];
+    r.valid[j] = mask[row * 192 + j * 64 + lane] != 0.f;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    if (r.valid[j]) mx = fmaxf(mx, x[j]);
+  mx = wmax(mx);
+  float e[3], se = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    e[j] = r.valid[j] ? expf(__fsub_rn(x[j], mx)) : 0.f;
+    se = __fadd_rn(se, e[j]);
+  }
+  se = wsum(se);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    r.p[j] = __fdiv_rn(e[j], se);
+    s = __fadd_rn(s, r.p[j]);
+  }
+  r.s = wsum(s);
+  const int aj = (int)(a >> 6), al = (int)(a & 63);
+  r.pa = __fdiv_rn(__shfl(aj == 0 ? r.p[0] : (aj == 1 ? r.p[1] : r.p[2]), al), r.s);
+  r.logp = logf(fminf(fmaxf(r.pa, kEps32), 1.f - kEps32));
+  float ms = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) ms = __fadd_rn(ms, r.valid[j] ? r.p[j] : 0.f);
+  r.ms_raw = wsum(ms);
+  r.ms = fmaxf(r.ms_raw, 1e-10f);
+  float h = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    r.q[j] = __fdiv_rn(r.valid[j] ? r.p[j] : 0.f, r.ms);
+    h = __fadd_rn(h, r.valid[j] ? __fmul_rn(r.q[j], logf(fmaxf(r.q[j], 1e-10f))) : 0.f);
+  }
+  r.ent = -wsum(h);
+}
+
+__global__ void __launch_bounds__(kLossThreads) ppo_loss_fwd_kernel(
+    const float* __restrict__ logits, const float* __restrict__ values, const float* __restrict__ mask,
+    const int64_t* __restrict__ actions, const float* __restrict__ old_logp, const float* __restrict__ adv,
+    const float* __restrict__ ret, int B, float clip, double* __restrict__ part) {
+  __shared__ double red[kStats][kRowsPerBlock];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double acc[kStats] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < B; row += (int64_t)gridDim.x * kRowsPerBlock) {
+    RowFwd r;
+    row_forward(logits, mask, row, actions[row], lane, r);
+    const float A = adv[row];
+    const float ratio = expf(__fsub_rn(r.logp, old_logp[row]));
+    const float s1 = __fmul_rn(ratio, A), s2 = __fmul_rn(fminf(fmaxf(ratio, 1.f - clip), 1.f + clip), A);
+    const float dv = __fsub_rn(values[row], ret[row]);
+    const float rm1 = __fsub_rn(ratio, 1.f);
+    acc[0] += (double)(-fminf(s1, s2));
+    acc[1] += (double)__fmul_rn(dv, dv);
+    acc[2] += (double)r.ent;
+    acc[3] += (double)__fsub_rn(rm1, logf(ratio));
+    acc[4] += fabsf(rm1) > clip ? 1.0 : 0.0;
+  }
+  if (lane == 0)
+    for (int k = 0; k < kStats; ++k) red[k][w] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < kStats) {
+    double t = 0.0;
+    for (int k = 0; k < kRowsPerBlock; ++k) t += red[threadIdx.x][k];
+    part[(int64_t)blockIdx.x * kStats + threadIdx.x] = t;
+  }
+}
+
+// stats = [policy_loss, value_loss, entropy, total_loss, approx_kl, clip_fraction]; loss = stats[3]
+__global__ void ppo_loss_finalize_kernel(const double* __restrict__ part, int nb, int B, float vcoef, float ecoef,
+                                         float* __restrict__ stats, float* __restrict__ loss) {
+  __shared__ double sh[kStats][64];
+  const int lane = threadIdx.x;  // one wave
+  double a[kStats] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int b = lane; b < nb; b += 64)
+    for (int k = 0; k < kStats; ++k) a[k] += part[(int64_t)b * kStats + k];
+  for (int k = 0; k < kStats; ++k) sh[k][lane] = a[k];
+  __syncthreads();
+  if (lane == 0) {
+    float m[kStats];
+    for (int k = 0; k < kStats; ++k) {
+      double t = 0.0;
+      for (int l = 0; l < 64; ++l) t += sh[k][l];
+      m[k] = (float)(t / (double)B);
+    }
+    const float total = __fadd_rn(__fadd_rn(m[0], __fmul_rn(vcoef, m[1])), __fmul_rn(ecoef, -m[2]));
+    stats[0] = m[0];
+    stats[1] = m[1];
+    stats[2] = m[2];
+    stats[3] = total;
+    stats[4] = m[3];
+    stats[5] = m[4];
+    if (loss) loss[0] = total;
+  }
+}
+
+__global__ void __launch_bounds__(kLossThreads) ppo_loss_bwd_kernel(
+    const float* __restrict__ logits, const float* __restrict__ values, const float* __restrict__ mask,
+    const int64_t* __restrict__ actions, const float* __restrict__ old_logp, const float* __restrict__ adv,
+    const float* __restrict__ ret, int B, float clip, float vcoef, float ecoef, const float* __restrict__ gloss,
+    float* __restrict__ dlogits, float* __restrict__ dvalues) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float g = gloss[0];
+  const float invB = 1.f / (float)B;
+  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < B; row += (int64_t)gridDim.x * kRowsPerBlock) {
+    const int64_t a = actions[row];
+    RowFwd r;
+    row_forward(logits, mask, row, a, lane, r);
+    const float A = adv[row];
+    const float ratio = expf(__fsub_rn(r.logp, old_logp[row]));
+    const float s1 = __fmul_rn(ratio, A), s2 = __fmul_rn(fminf(fmaxf(ratio, 1.f - clip), 1.f + clip), A);
+    // d loss / d min(s1, s2) = -g / B; torch.min splits ties half/half
+    const float gmin = -g * invB;
+    const float g1 = s1 < s2 ? gmin : (s1 > s2 ? 0.f : 0.5f * gmin);
+    const float g2 = s2 < s1 ? gmin : (s2 > s1 ? 0.f : 0.5f * gmin);
+    const bool in_clip = ratio >= 1.f - clip && ratio <= 1.f + clip;
+    const float glogp = (g1 * A + (in_clip ? g2 * A : 0.f)) * ratio;  // d exp(x)/dx = exp(x)
+    if (lane == 0) dvalues[row] = vcoef * g * invB * 2.f * __fsub_rn(values[row], ret[row]);  // mse_loss
+    const float gent = -ecoef * g * invB;  // ecoef * (-mean(ent))
+    // log(clamp(P_a, eps, 1 - eps)): passes where eps <= P_a <= 1 - eps, divided by the clamped value
+    const float gPa = (r.pa >= kEps32 && r.pa <= 1.f - kEps32) ? glogp / r.pa : 0.f;
+    // P = p / s: gp_k = [k == a] gPa / s - gPa p_a / s^2
+    const int aj = (int)(a >> 6), al = (int)(a & 63);
+    const float p_a = __shfl(aj == 0 ? r.p[0] : (aj == 1 ? r.p[1] : r.p[2]), al);
+    const float corr = gPa * p_a / (r.s * r.s);
+    // entropy = -sum m q log(clamp(q, 1e-10)), q = m p / clamp(ms, 1e-10):
+    //   d/dq_j = -m_j (log(clamp(q_j)) + [q_j >= 1e-10])
+    float gq[3], sgqm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      gq[j] = 0.f;
+      if (r.valid[j]) gq[j] = -gent * (logf(fmaxf(r.q[j], 1e-10f)) + (r.q[j] >= 1e-10f ? 1.f : 0.f));
+      sgqm += r.valid[j] ? gq[j] * r.p[j] : 0.f;
+    }
+    sgqm = wsum(sgqm);
+    const float gms = r.ms_raw >= 1e-10f ? -sgqm / (r.ms * r.ms) : 0.f;
+    float gp[3], dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      gp[j] = ((j == aj && lane == al) ? gPa / r.s : 0.f) - corr;
+      if (r.valid[j]) gp[j] += gq[j] / r.ms + gms;
+      dot += gp[j] * r.p[j];
+    }
+    dot = wsum(dot);
+    // softmax backward: dz_k = p_k (gp_k - sum_j gp_j p_j); masked entries have p = 0
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dlogits[row * 192 + j * 64 + lane] = r.p[j] * (gp[j] - dot);
+  }
+}
+
+int loss_blocks(int B) {
+  int b = (B + kRowsPerBlock - 1) / kRowsPerBlock;
+  return b < 1 ? 1 : (b > 4096 ? 4096 : b);
+}
+
+}  // namespace
+
+int64_t ppo_loss_workspace_bytes(int B) { return (int64_t)sizeof(double) * kStats * loss_blocks(B); }
+
+hipError_t launch_ppo_loss_forward(const float* logits, const float* values, const float* mask, const int64_t* actions,
+                                   const float* old_logp, const float* adv, const float* ret, int B, float clip,
+                                   float vcoef, float ecoef, double* ws, float* stats, float* loss, hipStream_t s) {
+  const int nb = loss_blocks(B);
+  hipLaunchKernelGGL(ppo_loss_fwd_kernel, dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask, actions, old_logp,
+                     adv, ret, B, clip, ws);
+  hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(64), 0, s, ws, nb, B, vcoef, ecoef, stats, loss);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_loss_backward(const float* logits, const float* values, const float* mask,
+                                    const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
+                                    int B, float clip, float vcoef, float ecoef, const float* gloss, float* dlogits,
+                                    float* dvalues, hipStream_t s) {
+  hipLaunchKernelGGL(ppo_loss_bwd_kernel, dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits, values, mask,
+                     actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues);
+  return hipGetLastError();
+}
+
+}  // namespace bb

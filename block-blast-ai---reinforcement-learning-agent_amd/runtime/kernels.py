@@ -180,3 +180,47 @@ class BatchNormReLUFunction(torch.autograd.Function):
                                         _p(dw), _p(db), _p(dpb), _s(dev)),
                 "bb_bn_backward")
         return dx, dpb, dw, db, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------------
+# PPO minibatch loss, forward and backward (csrc/bb_loss.hip)
+# ---------------------------------------------------------------------------
+class PPOLossFunction(torch.autograd.Function):
+    """PPOAgent's minibatch loss (ppo.py:362-401) with the masked Categorical
+    tail (network.py:173-180, 210-262) on bb_ppo_loss_forward/backward.
+    Returns (total loss, stats[6] = policy / value / entropy / total loss,
+    approx_kl, clip_fraction); stats carry no gradient."""
+
+    @staticmethod
+    def forward(ctx, logits, values, masks, actions, old_log_probs, advantages, returns, clip: float,
+                value_coef: float, entropy_coef: float):
+        _need_cuda(logits, values, masks, actions, old_log_probs, advantages, returns)
+        ins = (logits.contiguous().float(), values.contiguous().float(), masks.contiguous().float(),
+               actions.contiguous().long(), old_log_probs.contiguous().float(), advantages.contiguous().float(),
+               returns.contiguous().float())
+        b = ins[0].shape[0]
+        dev = ins[0].device
+        lib = L.load()
+        ws = torch.empty((lib.bb_ppo_loss_workspace_bytes(b) + 7) // 8, dtype=torch.float64, device=dev)
+        stats = torch.empty(6, dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        L.check(lib.bb_ppo_loss_forward(*[_p(t) for t in ins], b, float(clip), float(value_coef),
+                                        float(entropy_coef), _p(ws), _p(stats), _p(loss), _s(dev)),
+                "bb_ppo_loss_forward")
+        ctx.save_for_backward(*ins)
+        ctx.coef = (float(clip), float(value_coef), float(entropy_coef))
+        ctx.mark_non_differentiable(stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, grad_loss, grad_stats):
+        ins = ctx.saved_tensors
+        b = ins[0].shape[0]
+        dev = ins[0].device
+        g = grad_loss.float().reshape(1).contiguous()
+        dlogits = torch.empty_like(ins[0])
+        dvalues = torch.empty_like(ins[1])
+        L.check(L.load().bb_ppo_loss_backward(*[_p(t) for t in ins], b, *ctx.coef, _p(g), _p(dlogits), _p(dvalues),
+                                              _s(dev)),
+                "bb_ppo_loss_backward")
+        return dlogits, dvalues, None, None, None, None, None, None, None, None

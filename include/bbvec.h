@@ -268,6 +268,28 @@ int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhw
                    int32_t relu, double* d_ws, void* d_dx, float* d_dweight, float* d_dbias,
                    float* d_dpre_bias, void* stream);
 
+/* The PPO minibatch loss (PPOAgent.update, ppo.py:362-401) with the masked
+ * Categorical tail (network.py:173-180, 210-262), fused, forward and backward.
+ * Per row i < B: logits f32 [B][192] (raw policy head), mask f32 [B][192]
+ * (non-zero = legal), action, old log-prob, advantage, return and value.
+ * Forward writes d_stats[6] = {policy_loss, value_loss, entropy, total_loss,
+ * approx_kl, clip_fraction} (the reference's update metrics) and, if non-NULL,
+ * d_loss[0] = total_loss; d_ws is scratch of bb_ppo_loss_workspace_bytes(B)
+ * bytes.  Backward takes d(total_loss) from d_grad_loss[0] (device memory, so
+ * a HIP graph can replay it) and writes d/dlogits [B][192] and d/dvalues [B],
+ * following torch autograd's rules for min / clamp / log. */
+int64_t bb_ppo_loss_workspace_bytes(int32_t B);
+int bb_ppo_loss_forward(const float* d_logits, const float* d_values, const float* d_mask,
+                        const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                        const float* d_ret, int32_t B, float clip, float value_coef,
+                        float entropy_coef, double* d_ws, float* d_stats, float* d_loss,
+                        void* stream);
+int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const float* d_mask,
+                         const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                         const float* d_ret, int32_t B, float clip, float value_coef,
+                         float entropy_coef, const float* d_grad_loss, float* d_dlogits,
+                         float* d_dvalues, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

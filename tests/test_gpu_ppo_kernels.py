@@ -212,3 +212,44 @@ def test_network_fused_conv_bias_batchnorm_matches_torch(cuda, channels_last):
         assert rel < 5e-3, (name, rel)
     for (name, b), br in zip(net.named_buffers(), ref.buffers()):
         assert torch.allclose(b.float(), br.float(), rtol=1e-4, atol=1e-5), name
+
+
+@pytest.mark.parametrize("density", [0.02, 0.3, 1.0])
+def test_fused_ppo_loss_matches_torch(cuda, density):
+    """bb_ppo_loss_forward/backward (PPOLossFunction) vs the torch ops of
+    ppo.py:362-392 (agents.ppo.ppo_loss_torch), fp32: the loss, the six update
+    metrics, d/dlogits and d/dvalues.  Rows include single-legal-action masks
+    (P = 1: the log-prob clamps and passes no gradient), ratios inside and
+    outside the clip range, ratio-1 rows and zero advantages."""
+    from agents.ppo import PPOConfig, ppo_loss_torch
+    from runtime.kernels import PPOLossFunction
+
+    torch.manual_seed(int(density * 100))
+    B = 2048
+    cfg = PPOConfig()
+    logits = (torch.randn(B, 192, device=cuda) * 3).requires_grad_(True)
+    values = torch.randn(B, device=cuda).requires_grad_(True)
+    mask = (torch.rand(B, 192, device=cuda) < density).float()
+    mask[torch.arange(B, device=cuda), torch.randint(0, 192, (B,), device=cuda)] = 1.0
+    mask[:16] = 0.0
+    mask[:16, 5] = 1.0
+    actions = torch.multinomial(mask, 1).squeeze(1)
+    with torch.no_grad():
+        lp = torch.log_softmax(logits.masked_fill(mask == 0, float("-inf")), -1).gather(1, actions[:, None])[:, 0]
+    old = lp + torch.randn(B, device=cuda) * 0.3
+    old[16:32] = lp[16:32]
+    adv = torch.randn(B, device=cuda)
+    adv[32:40] = 0.0
+    ret = torch.randn(B, device=cuda)
+    lf, sf = PPOLossFunction.apply(logits, values, mask, actions, old, adv, ret, cfg.clip_epsilon, cfg.value_coef,
+                                   cfg.entropy_coef)
+    gl_f, gv_f = torch.autograd.grad(lf, [logits, values])
+    lr, sr = ppo_loss_torch(logits, values, mask, actions, old, adv, ret, cfg)
+    gl_r, gv_r = torch.autograd.grad(lr, [logits, values])
+    torch.testing.assert_close(lf, lr.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(sf[:5], sr[:5], rtol=1e-5, atol=1e-6)
+    assert abs(float(sf[5] - sr[5])) <= 2.0 / B  # a ratio on the clip boundary may round either way
+    torch.testing.assert_close(gv_f, gv_r, rtol=1e-5, atol=1e-9)
+    scale = float(gl_r.abs().max())
+    torch.testing.assert_close(gl_f, gl_r, rtol=1e-4, atol=1e-5 * scale)
+    assert float(gl_f[:16].abs().max()) <= 1e-5 * scale  # clamped log-prob + one-point entropy: no gradient
