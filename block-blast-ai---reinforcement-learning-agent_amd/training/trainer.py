@@ -188,6 +188,13 @@ def train(config: Dict[str, Any], resume_path: Optional[str] = None, seed: int =
     dirs = create_directories(config, make=main)
 
     ppo_cfg, train_cfg = config.get("ppo", {}), config.get("training", {})
+    # set_seed turns on cudnn.deterministic like the reference (device.py:74-90).  Under MIOpen
+    # that excludes the split-K weight-gradient convolutions and made a 65,536-env PPO update
+    # several times slower, so the trainer turns it back off unless training.deterministic is set;
+    # env streams, rollouts and sampling stay deterministic either way, only the CNN gradients'
+    # last bits vary run to run.
+    if torch.cuda.is_available():
+        torch.backends.cudnn.deterministic = bool(train_cfg.get("deterministic", False))
     reward_cfg, log_cfg = config.get("rewards", {}), config.get("logging", {})
     name = f"ppo_{datetime.now().strftime('%Y%m%d_%H%M%S')}"
     logger = Logger(str(dirs["log"]), name, enabled=main)

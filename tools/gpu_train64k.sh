@@ -10,6 +10,6 @@ W=$(mktemp -d)
 ( while sleep 30; do date +%T >> "$GRAFT_REPO_ROOT/gpurun_out/train64k_heartbeat.log"; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-sed "s#checkpoints#$W/ck#; s#logs#$W/logs#; s#results#$W/res#" config/${CFG:-gpu_64k_bf16}.yaml > $W/cfg.yaml
+sed "s#checkpoints#$W/ck#; s#logs#$W/logs#; s#results#$W/res#; s#num_envs: 65536#num_envs: ${ENVS:-65536}#" config/${CFG:-gpu_64k_bf16}.yaml > $W/cfg.yaml
 timeout -k 10 ${TL:-900} python -u run_train.py --config $W/cfg.yaml --max-updates ${UPD:-2} > "$GRAFT_REPO_ROOT/gpurun_out/train64k_${CFG:-gpu_64k_bf16}.log" 2>&1
 rc=$?; tail -25 "$GRAFT_REPO_ROOT/gpurun_out/train64k_${CFG:-gpu_64k_bf16}.log"; exit $rc
