@@ -212,60 +212,68 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
   }
 }
 
-// sums[c][m] = sum over nb blocks of part[blk][c][m]: one wave per channel.
-__global__ void __launch_bounds__(kBnThreads) bn_sum_partials(const double* __restrict__ part, int nb, int C,
-                                                              double* __restrict__ sums) {
-  const int c = blockIdx.x * (kBnThreads / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
-  double a[kQ] = {0.0, 0.0, 0.0};
-  for (int blk = lane; blk < nb; blk += 64)
-    for (int m = 0; m < kQ; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
-  for (int m = 0; m < kQ; ++m) a[m] = wave_sum(a[m]);
-  if (lane == 0)
-    for (int m = 0; m < kQ; ++m) sums[c * kQ + m] = a[m];
-}
-
 // Per-channel coefficients of the elementwise passes, packed 8 floats per
 // channel so an apply thread loads them as two 16-byte vectors:
 //   forward  {pre_bias, mean, invstd * weight, bias, -, -, -, -}
 //   backward {pre_bias, mean, invstd * weight, bias, invstd, mean(g), mean(g * xhat), -}
 constexpr int kCoef = 8;
 
-// Forward finalisation (one thread per channel): mean, inverse std of the
-// biased variance (the normalisation), running statistics with the unbiased
-// variance (nn.BatchNorm2d, momentum = exponential_average_factor), coefficients.
-__global__ void bn_finalize_fwd(int C, double M, const double* __restrict__ sums, float eps,
-                                const float* __restrict__ pre_bias, const float* __restrict__ w,
-                                const float* __restrict__ b, float* __restrict__ save_mean,
-                                float* __restrict__ save_invstd, float* __restrict__ rmean, float* __restrict__ rvar,
-                                float momentum, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const double m = sums[kQ * c] / M;
-  double var = sums[kQ * c + 1] / M - m * m;
+// The per-channel sums over the nb block partials part[blk][c][kQ], one wave
+// per channel (fixed order), valid in lane 0.
+__device__ __forceinline__ bool channel_sums(const double* __restrict__ part, int nb, int C, int& c, double a[kQ]) {
+  c = blockIdx.x * (kBnThreads / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return false;
+  a[0] = a[1] = a[2] = 0.0;
+  for (int blk = lane; blk < nb; blk += 64)
+    for (int m = 0; m < kQ; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
+  for (int m = 0; m < kQ; ++m) a[m] = wave_sum(a[m]);
+  return lane == 0;
+}
+
+// Forward finalisation: mean, inverse std of the biased variance (the
+// normalisation), running statistics with the unbiased variance
+// (nn.BatchNorm2d, momentum = exponential_average_factor), num_batches_tracked
+// += 1, coefficients.
+__global__ void __launch_bounds__(kBnThreads) bn_finalize_fwd(const double* __restrict__ part, int nb, int C, double M,
+                                                              float eps, const float* __restrict__ pre_bias,
+                                                              const float* __restrict__ w, const float* __restrict__ b,
+                                                              float* __restrict__ save_mean,
+                                                              float* __restrict__ save_invstd,
+                                                              float* __restrict__ rmean, float* __restrict__ rvar,
+                                                              float momentum, int64_t* __restrict__ nbt,
+                                                              float* __restrict__ coef) {
+  int c;
+  double a[kQ];
+  if (!channel_sums(part, nb, C, c, a)) return;
+  const double m = a[0] / M;
+  double var = a[1] / M - m * m;
   if (var < 0.0) var = 0.0;
   const float mu = (float)m, is = (float)(1.0 / sqrt(var + (double)eps));
   save_mean[c] = mu;
   save_invstd[c] = is;
   if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
   if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1.0 ? var * M / (M - 1.0) : var);
+  if (nbt && c == 0) nbt[0] += 1;
   float4* o = reinterpret_cast<float4*>(coef + kCoef * c);
   o[0] = make_float4(pre_bias ? pre_bias[c] : 0.f, mu, is * w[c], b[c]);
 }
 
-// Backward finalisation (one thread per channel): dweight = sum(g * xhat),
-// dbias = sum(g), the convolution bias gradient sum(dx) (dx = sc * (g - mg -
-// xhat * mgx) summed in fp64), coefficients.
-__global__ void bn_finalize_bwd(int C, double M, const double* __restrict__ sums, const float* __restrict__ pre_bias,
-                                const float* __restrict__ w, const float* __restrict__ b,
-                                const float* __restrict__ mean, const float* __restrict__ invstd,
-                                float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dpb,
-                                float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Backward finalisation: dweight = sum(g * xhat), dbias = sum(g), the
+// convolution bias gradient sum(dx) (dx = sc * (g - mg - xhat * mgx) summed in
+// fp64), coefficients.
+__global__ void __launch_bounds__(kBnThreads) bn_finalize_bwd(const double* __restrict__ part, int nb, int C, double M,
+                                                              const float* __restrict__ pre_bias,
+                                                              const float* __restrict__ w, const float* __restrict__ b,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, float* __restrict__ dw,
+                                                              float* __restrict__ db, float* __restrict__ dpb,
+                                                              float* __restrict__ coef) {
+  int c;
+  double a[kQ];
+  if (!channel_sums(part, nb, C, c, a)) return;
   const float invM = (float)(1.0 / M);
-  const double sg = sums[kQ * c], sgx = sums[kQ * c + 1], sx = sums[kQ * c + 2];
+  const double sg = a[0], sgx = a[1], sx = a[2];
   const float is = invstd[c], sc = is * w[c];
   const float mg = (float)sg * invM, mgx = (float)sgx * invM;
   if (dw) dw[c] = (float)sgx;
@@ -392,40 +400,37 @@ int grid_for_elems(int64_t chunks, int nhwc) {
 template <typename T, bool BWD>
 void launch_reduce(const Plan& p, int nhwc, const void* x, const void* dy, int N, int C, int HW, const float* pb,
                    const float* w, const float* b, const float* mean, const float* invstd, int relu, double* part,
-                   double* sums, hipStream_t s) {
+                   hipStream_t s) {
   if (nhwc)
     hipLaunchKernelGGL((bn_reduce_nhwc<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N * HW, C, pb, w, b, mean,
                        invstd, relu, part);
   else
     hipLaunchKernelGGL((bn_reduce_nchw<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N, C, HW, pb, w, b, mean,
                        invstd, relu, part);
-  hipLaunchKernelGGL(bn_sum_partials, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, part, p.nb, C, sums);
 }
 
 // Workspace (16-byte aligned): coefficients [C][kCoef] floats (float4 loads),
-// sums [C][kQ] doubles, partials [nb][C][kQ] doubles.
+// then the block partials [nb][C][kQ] doubles.
 struct Ws {
   float* coef;
-  double* sums;
   double* part;
 };
 Ws split_ws(double* ws, int C) {
   Ws w;
   w.coef = reinterpret_cast<float*>(ws);
-  w.sums = ws + kCoef / 2 * C;
-  w.part = w.sums + kQ * C;
+  w.part = ws + kCoef / 2 * C;
   return w;
 }
 
 template <typename T>
 hipError_t bn_forward_t(const void* x, int nhwc, int N, int C, int HW, const float* pb, const float* w,
                         const float* b, float eps, int relu, double* ws, float* save_mean, float* save_invstd,
-                        float* rmean, float* rvar, float momentum, void* y, hipStream_t s) {
+                        float* rmean, float* rvar, float momentum, int64_t* nbt, void* y, hipStream_t s) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
-  launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, k.part, k.sums, s);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 255) / 256), dim3(256), 0, s, C, (double)N * HW, k.sums, eps, pb, w,
-                     b, save_mean, save_invstd, rmean, rvar, momentum, k.coef);
+  launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, k.part, s);
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, k.part, p.nb, C, (double)N * HW, eps,
+                     pb, w, b, save_mean, save_invstd, rmean, rvar, momentum, nbt, k.coef);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
     hipLaunchKernelGGL((bn_apply_fwd<T, true>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, relu, k.coef);
@@ -440,9 +445,9 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
                          void* dx, float* dw, float* db, float* dpb, hipStream_t s) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
-  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, k.sums, s);
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 255) / 256), dim3(256), 0, s, C, (double)N * HW, k.sums, pb, w, b,
-                     mean, invstd, dw, db, dpb, k.coef);
+  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s);
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, k.part, p.nb, C, (double)N * HW, pb,
+                     w, b, mean, invstd, dw, db, dpb, k.coef);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
     hipLaunchKernelGGL((bn_apply_bwd<T, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
@@ -457,17 +462,18 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
 
 int64_t bn_workspace_bytes(int dtype, int nhwc, int N, int C, int HW) {
   const Plan p = plan_for(dtype == 1 ? 2 : 4, nhwc, N, C, HW);
-  return (int64_t)sizeof(double) * C * (kQ + kCoef / 2 + kQ * (int64_t)p.nb);
+  return (int64_t)sizeof(double) * C * (kCoef / 2 + kQ * (int64_t)p.nb);
 }
 
 hipError_t launch_bn_forward(const void* x, int dtype, int nhwc, int N, int C, int HW, const float* pb,
                              const float* w, const float* b, float eps, int relu, double* ws, float* save_mean,
-                             float* save_invstd, float* rmean, float* rvar, float momentum, void* y, hipStream_t s) {
+                             float* save_invstd, float* rmean, float* rvar, float momentum, int64_t* nbt, void* y,
+                             hipStream_t s) {
   if (dtype == 1)
     return bn_forward_t<__hip_bfloat16>(x, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean,
-                                        rvar, momentum, y, s);
+                                        rvar, momentum, nbt, y, s);
   return bn_forward_t<float>(x, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar, momentum,
-                             y, s);
+                             nbt, y, s);
 }
 
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,

@@ -46,9 +46,9 @@ class BatchNorm2d(nn.BatchNorm2d):
         if self.fusable(x):
             from runtime.kernels import BatchNormReLUFunction
 
-            self.num_batches_tracked.add_(1)
             return BatchNormReLUFunction.apply(x, pre_bias, self.weight, self.bias, self.running_mean,
-                                               self.running_var, self.momentum, self.eps, self.fuse_relu)
+                                               self.running_var, self.momentum, self.eps, self.fuse_relu,
+                                               self.num_batches_tracked)  # += 1 in the finalize kernel
         if pre_bias is not None:
             x = x + pre_bias.view(1, -1, 1, 1).to(x.dtype)
         y = super().forward(x)

@@ -145,7 +145,8 @@ class BatchNormReLUFunction(torch.autograd.Function):
     nn.BatchNorm2d [-> ReLU]; its gradient is the per-channel sum of dx."""
 
     @staticmethod
-    def forward(ctx, x, pre_bias, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool):
+    def forward(ctx, x, pre_bias, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool,
+                num_batches_tracked=None):
         nhwc = _bn_layout(x)
         x = x.contiguous(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         n, c, h, w = x.shape
@@ -156,7 +157,8 @@ class BatchNormReLUFunction(torch.autograd.Function):
         invstd = torch.empty(c, dtype=torch.float32, device=dev)
         L.check(L.load().bb_bn_forward(_p(x), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight),
                                        _p(bias), float(eps), int(relu), _p(ws), _p(mean), _p(invstd),
-                                       _p(running_mean), _p(running_var), float(momentum), _p(y), _s(dev)),
+                                       _p(running_mean), _p(running_var), float(momentum), _p(num_batches_tracked),
+                                       _p(y), _s(dev)),
                 "bb_bn_forward")
         ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd)
         ctx.relu = bool(relu)
@@ -179,7 +181,7 @@ class BatchNormReLUFunction(torch.autograd.Function):
                                         _p(weight), _p(bias), _p(mean), _p(invstd), int(ctx.relu), _p(ws), _p(dx),
                                         _p(dw), _p(db), _p(dpb), _s(dev)),
                 "bb_bn_backward")
-        return dx, dpb, dw, db, None, None, None, None, None
+        return dx, dpb, dw, db, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------

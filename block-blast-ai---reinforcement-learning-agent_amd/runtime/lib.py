@@ -131,7 +131,8 @@ SIGNATURES = {
     "bb_gae": (C.c_int, [_P, _P, _P, _P, _I32, _I32, _F, _F, _P, _P, _P]),
     "bb_gather_obs": (C.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P]),
     "bb_bn_workspace_bytes": (C.c_int64, [_I32, _I32, _I32, _I32, _I32]),
-    "bb_bn_forward": (C.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _F, _P, _P]),
+    "bb_bn_forward": (C.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _F, _P, _P,
+                                _P]),
     "bb_bn_backward": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                  _P]),
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),

@@ -250,7 +250,8 @@ int bb_gather_obs(const uint64_t* d_board, const uint32_t* d_hand,
  * element size = 16 bytes times a power of two <= 256); weight / bias /
  * statistics are f32.  Forward = nn.BatchNorm2d training forward (batch mean,
  * biased variance for the normalisation; running_mean / running_var updated
- * with `momentum` and the unbiased variance when non-NULL), then max(y, 0) if
+ * with `momentum` and the unbiased variance when non-NULL, num_batches_tracked
+ * incremented when non-NULL), then max(y, 0) if
  * relu.  d_ws is caller scratch of bb_bn_workspace_bytes(...) bytes (16-byte
  * aligned).  Backward takes the forward's input x and saved mean / inverse
  * std; with relu it recomputes the mask from x.  It writes dx and, where
@@ -261,7 +262,7 @@ int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32_t N, int32
                   const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps,
                   int32_t relu, double* d_ws, float* d_save_mean, float* d_save_invstd,
                   float* d_running_mean, float* d_running_var, float momentum,
-                  void* d_y, void* stream);
+                  int64_t* d_num_batches_tracked, void* d_y, void* stream);
 int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N,
                    int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                    const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
