@@ -40,9 +40,13 @@ constexpr int kStepBlock = BB_STEP_BLOCK;
 #endif
 constexpr int kEscBlock = BB_ESC_BLOCK;
 #ifndef BB_ESC_GROUP
-#define BB_ESC_GROUP 8
+#define BB_ESC_GROUP 32  // with the multi-env search: 8 -> 32 took the step tail from 71 to 68 us
 #endif
-constexpr int kEscGroup = BB_ESC_GROUP;  // envs owned by one escalation wave
+constexpr int kEscGroup = BB_ESC_GROUP;  // envs owned by one escalation wave (< 64)
+static_assert(kEscGroup > 0 && kEscGroup < 64, "gen_hands_multi masks (1 << kEnvs) - 1");
+#ifndef BB_ESC_MULTI
+#define BB_ESC_MULTI 1  // escalate_kernel: parked envs searched together; 0: one env at a time
+#endif
 
 constexpr int kDPad = (kPieces * kPieces + 15) / 16 * 16;  // |D| table padded to whole 16-byte vectors
 
@@ -500,8 +504,23 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
   }
   stage_tables(t, g_rows, g_d);  // most escalate blocks find nothing parked: no jump table in LDS
   if (!parked) return;
-  // one parked env at a time, searched by the whole wave (register broadcast)
   uint32_t my_ids = 0;
+#if BB_ESC_MULTI
+  // the parked envs of this wave searched together, attempts of several envs
+  // packed into one pass (gen_hands_multi, as in rollout_kernel); the step
+  // kernel's attempts count against each env's 100 (engine.py:159-172)
+  if (!(a.dbg & 2)) {
+    gen_hands_multi<kEscGroup>(parked, s.B, s.rng, my_ids, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next,
+                               scratch + (threadIdx.x & ~63), nullptr, (int)(pr & 0xFFu));
+    if (flagged) {
+      s.hand = my_ids | ((uint32_t)s.rng.has << 22);
+      finalize(t, e, s, a);
+      e.pend[mine] = 0;
+    }
+    return;
+  }
+#endif
+  // one parked env at a time, searched by the whole wave (register broadcast)
   uint64_t it = parked;
   while (it) {
     const int k = __ffsll((unsigned long long)it) - 1;

@@ -736,10 +736,11 @@ template <int kEnvs>
 __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pcg& rng, uint32_t& ids,
                                                 const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
                                                 int lane, int pack_first, int pack_next, uint32_t* lds,
-                                                uint64_t* prof = nullptr) {  // diagnostics: [6] cycle sums
+                                                uint64_t* prof = nullptr,  // diagnostics: [6] cycle sums
+                                                int att0 = 0) {  // attempts an earlier pass consumed (env lanes)
 #define BB_MT(x) const uint64_t x = prof ? __builtin_amdgcn_s_memtime() : 0
   const int me = lane % kEnvs;  // env index held by this lane
-  int att = 0;                // attempts consumed so far (env lanes)
+  int att = att0;             // attempts consumed so far (env lanes)
   uint32_t last_ids = 0;      // last drawn hand, kept after 100 failures (engine.py:171-172)
   uint64_t todo = parked;
   int round = 0;
