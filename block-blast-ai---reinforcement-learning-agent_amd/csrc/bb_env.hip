@@ -14,9 +14,10 @@
 //                      auto-reset, action mask and the fused random policy.
 //                      Envs whose hand search ran out of budget are parked:
 //                      post-move state + a pending flag.
-//   escalate_kernel -- each wave owns 16 envs; every parked env is finished by
-//                      its whole wave (lane-parallel over level-1 anchors) and
-//                      then finalised exactly like step_kernel would have.
+//   escalate_kernel -- each wave owns 32 envs; its parked envs are searched
+//                      together by the whole wave (gen_hands_multi: attempts of
+//                      several envs packed into 64-lane passes) and then
+//                      finalised exactly like step_kernel would have.
 // Spreading the rare hard boards over 4x more waves than the step kernel
 // keeps the slowest wave short.
 //
@@ -46,6 +47,9 @@ constexpr int kEscGroup = BB_ESC_GROUP;  // envs owned by one escalation wave (<
 static_assert(kEscGroup > 0 && kEscGroup < 64, "gen_hands_multi masks (1 << kEnvs) - 1");
 #ifndef BB_ESC_MULTI
 #define BB_ESC_MULTI 1  // escalate_kernel: parked envs searched together; 0: one env at a time
+#endif
+#ifndef BB_ESC_LDS_JUMP
+#define BB_ESC_LDS_JUMP 0  // escalate_kernel (multi): PCG64 jump table staged in LDS
 #endif
 
 constexpr int kDPad = (kPieces * kPieces + 15) / 16 * 16;  // |D| table padded to whole 16-byte vectors
@@ -502,7 +506,15 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
     s.cm = (int)((pr >> 24) & 0xFFu);
     s.gained = (int64_t)(uint32_t)(pr >> 32);
   }
-  stage_tables(t, g_rows, g_d);  // most escalate blocks find nothing parked: no jump table in LDS
+#if BB_ESC_MULTI && BB_ESC_LDS_JUMP
+  // 32-env waves nearly always hold a parked env: the jump table goes to LDS too
+  __shared__ JumpRow jt[kJumpMax + 1];
+  stage_tables<true>(t, g_rows, g_d, jt, a.jump);
+  const JumpRow* J = jt;
+#else
+  stage_tables(t, g_rows, g_d);  // small groups mostly find nothing parked: no jump table in LDS
+  const JumpRow* J = a.jump;
+#endif
   if (!parked) return;
   uint32_t my_ids = 0;
 #if BB_ESC_MULTI
@@ -510,7 +522,7 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
   // packed into one pass (gen_hands_multi, as in rollout_kernel); the step
   // kernel's attempts count against each env's 100 (engine.py:159-172)
   if (!(a.dbg & 2)) {
-    gen_hands_multi<kEscGroup>(parked, s.B, s.rng, my_ids, t.row, t.d, a.jump, lane, a.pack_first, a.pack_next,
+    gen_hands_multi<kEscGroup>(parked, s.B, s.rng, my_ids, t.row, t.d, J, lane, a.pack_first, a.pack_next,
                                scratch + (threadIdx.x & ~63), nullptr, (int)(pr & 0xFFu));
     if (flagged) {
       s.hand = my_ids | ((uint32_t)s.rng.has << 22);
