@@ -4,12 +4,15 @@
 Default workload (BASELINE config 2, one GPU): 65,536 envs per GPU, env i
 seeded 42 + global index, HIP bitboard step + action mask + in-kernel
 auto-reset, actions from the synthetic random policy (Philox, fused into the
-kernel).  One "step" = one env-step of the whole batch.  The default
-`--mode rollout` runs T = 128 steps (the reference's PPO horizon) per
-bb_rollout launch with the env state held in registers; `--mode step` runs
-one bb_step launch (step + escalate kernels) per step, the drop-in path under
-VectorizedBlockBlastEnv.step.  Both produce identical trajectories
-(tests/test_gpu_rollout.py).
+kernel).  A bench "step" is one pass of the hot path over one batch:
+  --mode rollout (default): one bb_rollout launch = T = 128 env-steps (the
+      reference's PPO horizon, scripts/train.py:173-203 / config n_steps) of
+      every env, the env state held in registers between its T steps;
+  --mode step: one bb_step launch (step + escalate kernels) = one env-step of
+      every env, the drop-in path under VectorizedBlockBlastEnv.step.
+Both produce identical trajectories (tests/test_gpu_rollout.py).  `value`
+counts env-steps (envs x T x K in rollout mode, envs x K in step mode) over
+the timed wall time.
 
     python bench.py --gpus N --steps K --warmup W [--mode rollout|step]
     (N > 1: launched by torch.distributed.run, one rank per GPU; envs are
@@ -92,8 +95,9 @@ def load_traffic(n_envs: int, mode: str, steps_per_launch: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed bench steps: bb_rollout launches of T env-steps (rollout) or bb_step launches (step)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -155,6 +159,7 @@ def main() -> None:
     step_idx = [0]
 
     def one_step(k=1):
+        """k bench steps: k bb_step launches (step mode) or k bb_rollout launches of T env-steps each."""
         t = step_idx[0]
         if args.mode == "step":
             for j in range(k):
@@ -165,18 +170,15 @@ def main() -> None:
         cur = torch.cuda.current_stream(dev)
         for _, st, _, _ in shards:
             st.wait_stream(cur)
-        done = 0
-        while done < k:  # T steps per launch, the action double-buffer flips once per launch
-            c = min(T, k - done)
+        for j in range(k):  # the action double-buffer flips once per launch
             for e, st, a, (o_rew, o_term, o_lines, o_act, o_mask) in shards:
                 with torch.cuda.stream(st):
-                    e.rollout(c, a[0], o_rew, o_term, lines=o_lines, actions_out=o_act, mask_out=o_mask,
-                              next_action=a[1], policy_seed=POLICY_SEED, policy_step0=t + done)
+                    e.rollout(T, a[0], o_rew, o_term, lines=o_lines, actions_out=o_act, mask_out=o_mask,
+                              next_action=a[1], policy_seed=POLICY_SEED, policy_step0=t + j * T)
                 a.reverse()
-            done += c
         for _, st, _, _ in shards:
             cur.wait_stream(st)
-        step_idx[0] = t + k
+        step_idx[0] = t + k * (1 if args.mode == "step" else T)
 
     one_step(args.warmup)
 
@@ -195,9 +197,9 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    # average launch: bb_step (both kernels + their gap) or one full T-step bb_rollout
+    # average launch (= one bench step): bb_step (both kernels + their gap) or one T-step bb_rollout
     per_launch = 1 if args.mode == "step" else T
-    kern_ms = ev0.elapsed_time(ev1) / args.steps * per_launch
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device="cpu" if share else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -208,7 +210,7 @@ def main() -> None:
         last_rew = e.reward if args.mode == "step" else outs[0]
         assert bool((last_rew != -10.0).all()), "random policy produced an illegal action"
 
-    total_env_steps = n * world * args.steps
+    total_env_steps = n * world * args.steps * per_launch
     value = total_env_steps / el
     if rank == 0:
         algo_bytes = ALGO_BYTES_PER_ENV_STEP * n * per_launch
@@ -231,6 +233,9 @@ def main() -> None:
                 "workload": "BASELINE config 2: 65,536 envs per MI355X, HIP bitboard step + action mask + "
                             "auto-reset, random policy (env throughput)",
                 "mode": args.mode if args.mode == "step" else f"rollout T={T}",
+                "bench_step": ("one bb_step launch = 1 env-step of every env" if args.mode == "step" else
+                               f"one bb_rollout launch = {T} env-steps of every env (the PPO horizon)"),
+                "env_steps_per_bench_step": n * world * per_launch,
                 "envs_per_gpu": n,
                 "global_envs": n * world,
                 "parallelism": f"env shards x{world} (no data-path collective)",
