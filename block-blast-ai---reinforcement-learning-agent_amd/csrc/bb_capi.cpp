@@ -25,7 +25,6 @@ struct bb_env {
   PieceRow* d_rows = nullptr;
   uint8_t* d_dtab = nullptr;
   JumpRow* d_jump = nullptr;
-  uint32_t* d_prog = nullptr;
   void* slab = nullptr;
   int lane_budget = 16; // in-lane search budget before parking (BB_LANE_BUDGET; 0 = park every draw)
   int lane_quick = 2;   // in-lane test of 2 fixed slots (BB_LANE_QUICK; 0 = budget search instead)
@@ -89,7 +88,6 @@ size_t slab_bytes(int n) {
   add(n, 1);      // has_seed
   add(n, 1);      // pend
   add(n, 8);      // pscratch
-  add(kProgSlots, 4);  // rollout progress words, one per SIMD wave slot
   add(kPieces, sizeof(PieceRow));
   add(kPieces * kPieces, 1);
   add(kJumpMax + 1, sizeof(JumpRow));
@@ -182,7 +180,6 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   carve(cur, d.has_seed, n);
   carve(cur, d.pend, n);
   carve(cur, d.pscratch, n);
-  carve(cur, e->d_prog, kProgSlots);
   carve(cur, e->d_rows, kPieces);
   carve(cur, e->d_dtab, kPieces * kPieces);
   carve(cur, e->d_jump, kJumpMax + 1);
@@ -307,7 +304,6 @@ int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions, const bb_ro
   r.mask = out->mask;
   r.next_action = out->next_action;
   r.policy_step0 = out->policy_step0;
-  r.prog = env->d_prog;
   DeviceGuard g(env->device);
   hipError_t st = launch_rollout(env->d, env->d_rows, env->d_dtab, a, r, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(env, st, "bb_rollout");

@@ -114,7 +114,8 @@ struct Pcg {
   uint64_t hi, lo;        // 128-bit LCG state
   uint64_t inc_hi, inc_lo;
   uint32_t buf;           // buffered upper 32-bit half (numpy `uinteger`)
-  bool has;               // numpy `has_uint32`
+  uint32_t has;           // numpy `has_uint32` (0/1); a full word: no padding bytes, which the
+                          // compiler otherwise round-trips through scratch on every struct copy
 };
 
 __device__ __forceinline__ uint64_t pcg_next64(Pcg& s) {
@@ -132,11 +133,11 @@ __device__ __forceinline__ uint64_t pcg_next64(Pcg& s) {
 
 __device__ __forceinline__ uint32_t pcg_next32(Pcg& s) {
   if (s.has) {
-    s.has = false;
+    s.has = 0u;
     return s.buf;
   }
   uint64_t v = pcg_next64(s);
-  s.has = true;
+  s.has = 1u;
   s.buf = (uint32_t)(v >> 32);
   return (uint32_t)v;
 }

@@ -75,26 +75,28 @@ __device__ __forceinline__ void stage_tables(Tables& t, const PieceRow* g_rows, 
   constexpr int kTabVec = kRowVec + kDPad / 16;
   constexpr int kTot = kTabVec + (kWithJump ? kJumpVec : 0);
   constexpr int kPer = (kTot + 63) / 64;
-  const uint4* rs = reinterpret_cast<const uint4*>(g_rows);
-  const uint4* ds = reinterpret_cast<const uint4*>(g_d);
-  const uint4* js = reinterpret_cast<const uint4*>(g_jump);
-  uint4* rd = reinterpret_cast<uint4*>(t.row);
-  uint4* dd = reinterpret_cast<uint4*>(t.d);
-  uint4* jd = reinterpret_cast<uint4*>(jt);
   const int tid = threadIdx.x;
+  const int nthr = (int)blockDim.x;
+  // one source / destination address per vector (a single select each), so the
+  // staged values stay in registers (a pointer select per load put them in scratch)
   uint4 v[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int idx = tid + k * (int)blockDim.x;
-    if (idx < kTot) v[k] = idx < kRowVec ? rs[idx] : (idx < kTabVec ? ds[idx - kRowVec] : js[idx - kTabVec]);
+    const int idx = tid + k * nthr;
+    const int j = idx < kTot ? idx : 0;
+    const char* src = j < kRowVec ? reinterpret_cast<const char*>(g_rows) + 16 * j
+                    : j < kTabVec ? reinterpret_cast<const char*>(g_d) + 16 * (j - kRowVec)
+                                  : reinterpret_cast<const char*>(g_jump) + 16 * (j - kTabVec);
+    v[k] = *reinterpret_cast<const uint4*>(src);
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int idx = tid + k * (int)blockDim.x;
+    const int idx = tid + k * nthr;
     if (idx < kTot) {
-      if (idx < kRowVec) rd[idx] = v[k];
-      else if (idx < kTabVec) dd[idx - kRowVec] = v[k];
-      else jd[idx - kTabVec] = v[k];
+      char* dst = idx < kRowVec ? reinterpret_cast<char*>(t.row) + 16 * idx
+                : idx < kTabVec ? reinterpret_cast<char*>(t.d) + 16 * (idx - kRowVec)
+                                : reinterpret_cast<char*>(jt) + 16 * (idx - kTabVec);
+      *reinterpret_cast<uint4*>(dst) = v[k];
     }
   }
   __syncthreads();
@@ -189,7 +191,7 @@ __device__ __forceinline__ void reset_lane(const Tables& t, bool has_seed, uint6
     rng.hi = seed_hi;
     rng.lo = seed_lo;
     rng.buf = 0;
-    rng.has = false;
+    rng.has = 0u;
   }
   B = 0;
   // Every one of the 37^3 hands fits an empty board (checked exhaustively
@@ -594,7 +596,7 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
 constexpr int kRollEnvs = BB_ROLL_ENVS;  // 32 (two copies per env) or 16 (four)
 static_assert(kRollEnvs == 16 || kRollEnvs == 32, "envs per wave");
 #ifndef BB_ROLL_BLOCK
-#define BB_ROLL_BLOCK 64
+#define BB_ROLL_BLOCK 512  // 8 waves: at 65,536 envs one workgroup per CU, both waves of a SIMD in it
 #endif
 constexpr int kRollBlock = BB_ROLL_BLOCK;
 #ifndef BB_ROLL_MINW
@@ -652,7 +654,24 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     m[1] = e.mask[3 * i + 1];
     m[2] = e.mask[3 * i + 2];
   }
-  stage_tables<true>(t, g_rows, g_d, jt, a.jump);
+  // The two waves on a SIMD issue by priority, then age: the older one runs
+  // nearly unimpeded and the younger one finishes up to 1.3x later, which
+  // sets the launch time.  Partners (same workgroup, same SIMD) publish their
+  // step counters in LDS; the one behind takes the higher priority.
+  constexpr int kWaves = kRollBlock / 64;
+  __shared__ uint32_t wave_simd[kWaves];
+  __shared__ uint32_t prog[kWaves];
+  const int wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    wave_simd[wv] = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;  // HW_ID.SIMD_ID
+    prog[wv] = 0u;
+  }
+  stage_tables<true>(t, g_rows, g_d, jt, a.jump);  // ends with __syncthreads
+  int pw = wv;  // partner wave: the other wave of this workgroup on this SIMD (itself if none)
+#pragma unroll
+  for (int k = 0; k < kWaves; ++k)
+    if (k != wv && wave_simd[k] == wave_simd[wv]) pw = k;
+  const uint32_t tie = wv < pw ? 1u : 0u;
   if (__ballot(live) == 0ull) return;  // wave-uniform
   if (live) s.rng.has = hand_has32(s.hand);
   // A seeded env re-seeds with seed_value on every reset (block_blast_env.py:212-215), so its
@@ -678,16 +697,6 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #else
 #define BB_DIAG_T(x)
 #endif
-  // The two waves on a SIMD issue by priority, then age: the older one runs
-  // nearly unimpeded and the younger one finishes up to 1.3x later, which
-  // sets the launch time.  They alternate the higher priority every step
-  // (HW_ID wave slot parity differs between the two).
-  const uint32_t hwid = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-  const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // XCC_ID
-  const uint32_t wslot = hwid & 15u;
-  const uint32_t simd_key = (xcc << 12) | ((hwid >> 4) & 0xFFFu);
-  uint32_t* my_prog = r.prog + simd_key * 16u + wslot;
-  const uint32_t* partner_prog = r.prog + simd_key * 16u + (wslot ^ 1u);
   uint32_t partner = 0;
   // The policy uniforms are shared by an env's copies: on every kCopies-th
   // step copy c draws the uniform of step + 1 + c, and each step reads its
@@ -697,16 +706,15 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #pragma unroll 1
   for (int step = 0; step < r.steps; ++step) {
 #if BB_ROLL_FAIR == 1
-    if (((uint32_t)step ^ wslot) & 1u) __builtin_amdgcn_s_setprio(1);
+    if (((uint32_t)step ^ tie) & 1u) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 #elif BB_ROLL_FAIR == 2
-    {  // the wave behind its SIMD partner (global step counters) takes the priority
-      const uint32_t mine = (uint32_t)(r.policy_step0 + (uint64_t)step);
-      const int32_t lead = (int32_t)(mine - partner);
-      if (lead < 0 || (lead == 0 && (((uint32_t)step ^ wslot) & 1u))) __builtin_amdgcn_s_setprio(1);
+    {  // the wave behind its SIMD partner (LDS step counters) takes the priority
+      const int32_t lead = step - (int32_t)partner;
+      if (lead < 0 || (lead == 0 && (((uint32_t)step ^ tie) & 1u))) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
-      if (lane == 0) __hip_atomic_store(my_prog, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      partner = __hip_atomic_load(partner_prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // used next step
+      if (lane == 0) __hip_atomic_store(&prog[wv], (uint32_t)step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      partner = __hip_atomic_load(&prog[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // used next step
     }
 #endif
     BB_DIAG_T(c0);

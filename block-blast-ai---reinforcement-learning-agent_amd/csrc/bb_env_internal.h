@@ -71,10 +71,7 @@ struct RollArgs {
   uint64_t* mask;               // [T][N][3] optional: post-step mask bits
   int32_t* next_action;         // [N] optional: policy action after the last step
   uint64_t policy_step0;        // step t's next action uses policy_step0 + t + 1
-  uint32_t* prog;               // [kProgSlots] per-SIMD-wave-slot step counters (scheduling only)
 };
-// One progress word per (XCC, SE, SH, CU, SIMD, wave slot): HW_ID bits 4-15 + wave id + XCC id.
-constexpr int kProgSlots = 8 * 4096 * 16;
 
 hipError_t launch_reset(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const uint8_t* sel, hipStream_t s);
 hipError_t launch_step(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const int32_t* actions,

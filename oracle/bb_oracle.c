@@ -342,7 +342,11 @@ static void generate(Engine* e, uint64_t* hist) {
     for (int k = 0; k < HAND; ++k) e->hand[k] = (int)draw_below(&e->rng, NPIECES);
     e->used[0] = e->used[1] = e->used[2] = 0;
     e->last_attempts = attempt + 1;
-    if (can_place_remaining(e->hand, &e->board, 0)) {
+    const int ok = can_place_remaining(e->hand, &e->board, 0);
+#ifdef BBO_GEN_HOOK /* analysis builds only (tools/search_stats.c) */
+    BBO_GEN_HOOK(e, attempt, ok);
+#endif
+    if (ok) {
       if (hist) hist[attempt] += 1;
       return;
     }

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Diagnostics (not product): tuning builds of libbbvec.so, recorded here so
+every A/B number in DESIGN.md can be rebuilt from the repo.
+
+    python tools/variants.py build NAME [NAME ...]   -> tools/variants/libbbvec_NAME.so
+    python tools/variants.py list
+
+Load one with BBVEC_LIB=tools/variants/libbbvec_NAME.so (runtime/lib.py).
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd", "csrc")
+OUT = os.path.join(REPO, "tools", "variants")
+SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_nn.hip", "bb_loss.hip", "bb_capi.cpp", "bb_tables.cpp"]
+
+VARIANTS = {
+    # name: extra -D flags on top of the shipped build (runtime/build.py)
+    "main": [],
+    # rollout kernel workgroup shape (waves per workgroup; SIMD partners share LDS progress words at 512)
+    "rblk64": ["-DBB_ROLL_BLOCK=64"],
+    "rblk256": ["-DBB_ROLL_BLOCK=256"],
+    # rollout SIMD-partner priority: 0 none, 1 alternate per step, 2 the wave behind takes it (shipped)
+    "fair0": ["-DBB_ROLL_FAIR=0"],
+    "fair1": ["-DBB_ROLL_FAIR=1"],
+    # round-1 escalate variants (their flags were not recorded)
+    "esc0": ["-DBB_ESC_MULTI=0", "-DBB_ESC_GROUP=8"],
+    "escg16": ["-DBB_ESC_GROUP=16"],
+    "escj": ["-DBB_ESC_LDS_JUMP=1"],
+    "escjb128": ["-DBB_ESC_LDS_JUMP=1", "-DBB_ESC_BLOCK=128"],
+    "escb128": ["-DBB_ESC_BLOCK=128"],
+    # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
+    "diag3": ["-DBB_ROLL_DIAG=3"],
+}
+
+
+def build(name: str) -> str:
+    flags = VARIANTS[name]
+    os.makedirs(OUT, exist_ok=True)
+    out = os.path.join(OUT, f"libbbvec_{name}.so")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
+           "-shared", "-Wno-unused-result", *flags, f"-I{os.path.join(REPO, 'include')}",
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+def main():
+    if len(sys.argv) < 2 or sys.argv[1] == "list":
+        for k, v in VARIANTS.items():
+            print(f"{k:12s} {' '.join(v)}")
+        return
+    names = sys.argv[2:]
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        for out in ex.map(build, names):
+            print(out)
+
+
+if __name__ == "__main__":
+    main()
