@@ -32,12 +32,23 @@ struct bb_env {
   int pack_next = 32;
   int dbg = 0;
   uint64_t* dbg_out = nullptr;
+  // set when a bb_step launch failed: step_kernel may have parked envs (pend=1,
+  // half-applied state) that escalate_kernel never finished; only a full
+  // bb_reset (which clears every pend flag) makes the handle usable again
+  bool broken = false;
   std::string err;
 };
 
 static thread_local std::string g_create_err;
 
 namespace {
+
+int fail(bb_env* e, int code, const std::string& msg);
+
+int broken_fail(bb_env* e, const char* what) {
+  return fail(e, BB_ERR_STATE, std::string(what) + ": an earlier bb_step launch failed and left parked envs; "
+                               "call bb_reset on all envs (d_env_mask = NULL) first");
+}
 
 int fail(bb_env* e, int code, const std::string& msg) {
   if (e) e->err = msg;
@@ -257,9 +268,11 @@ int bb_seed(bb_env* env, const uint64_t* h_seeds, const uint8_t* h_has_seed, con
 
 int bb_reset(bb_env* env, const uint8_t* d_env_mask, void* stream) {
   if (!env) return BB_ERR_ARG;
+  if (env->broken && d_env_mask) return broken_fail(env, "bb_reset (masked)");
   DeviceGuard g(env->device);
   hipError_t st = launch_reset(env->d, env->d_rows, env->d_dtab, d_env_mask, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(env, st, "bb_reset");
+  env->broken = false;  // every env reset, every pend flag cleared
   return BB_OK;
 }
 
@@ -279,8 +292,12 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.policy_step = out->policy_step;
   a.env_offset = out->env_offset;
   DeviceGuard g(env->device);
+  if (env->broken) return broken_fail(env, "bb_step");
   hipError_t st = launch_step(env->d, env->d_rows, env->d_dtab, d_actions, a, (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(env, st, "bb_step");
+  if (st != hipSuccess) {
+    env->broken = true;
+    return hip_fail(env, st, "bb_step");
+  }
   return BB_OK;
 }
 
@@ -290,6 +307,7 @@ int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions, const bb_ro
   if (!d_actions || !out || !out->reward || !out->terminated)
     return fail(env, BB_ERR_ARG, "bb_rollout: actions, reward and terminated are required");
   if (env->dbg & ~16) return fail(env, BB_ERR_STATE, "bb_rollout: only BB_DEBUG_MODE=16 (rollout phase counters)");
+  if (env->broken) return broken_fail(env, "bb_rollout");
   if (steps == 0) return BB_OK;
   StepArgs a = base_args(env);
   a.policy_seed = out->policy_seed;

@@ -743,12 +743,13 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
   int att = att0;             // attempts consumed so far (env lanes)
   uint32_t last_ids = 0;      // last drawn hand, kept after 100 failures (engine.py:171-172)
   uint64_t todo = parked;
-  int round = 0;
+  // attempts per env in this round: pack_first, then pack_next (0: double the
+  // previous round's, as gen_hand_wave does), capped at kPack
+  int pk = pack_first < kPack ? pack_first : kPack;
 #pragma unroll 1
   while (todo) {
     BB_MT(p0);
     const int E = __popcll(todo);
-    const int pk = round == 0 ? pack_first : pack_next;
     int K = 64 / E;
     K = K < pk ? K : pk;
     K = K < kPack ? K : kPack;
@@ -909,7 +910,8 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       }
     }
     todo &= ~(__ballot(done && lane < kEnvs) & ((1ull << kEnvs) - 1ull));
-    ++round;
+    pk = pack_next > 0 ? pack_next : 2 * pk;
+    pk = pk < kPack ? pk : kPack;
     if (prof) {
       BB_MT(p4);
       prof[0] += p1 - p0;  // batch setup + jump draws

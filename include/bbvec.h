@@ -148,7 +148,10 @@ int bb_reset(bb_env* env, const uint8_t* d_env_mask, void* stream);
 
 /* One step of every env with actions d_actions[N] (int32 flat actions):
  * VectorizedBlockBlastEnv.step (wrappers.py:75-116) -> BlockBlastEnv.step
- * (block_blast_env.py:224-264) -> GameEngine.make_move (engine.py:390-454). */
+ * (block_blast_env.py:224-264) -> GameEngine.make_move (engine.py:390-454).
+ * If a launch fails, the handle refuses bb_step / bb_rollout / masked
+ * bb_reset with BB_ERR_STATE until a full bb_reset (d_env_mask NULL): the
+ * step kernel may already have parked envs whose search never ran. */
 int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out,
             void* stream);
 
@@ -201,7 +204,12 @@ int bb_set_state(bb_env* env, const bb_state_view* h_view);
 /* Diagnostics: per-env hand-search counters of the last bb_step, [N][4] =
  * {in-lane cycles, attempts | escalated << 32, wave cycles, board}.  Only
  * available when the env was created with BB_DEBUG_MODE having bit 1 set;
- * reading clears them. */
+ * reading clears them.  NOTE: BB_DEBUG_MODE bit 1 (value 2) also switches the
+ * escalate kernel from the shipped multi-env search (gen_hands_multi) to the
+ * one-env-at-a-time wave search (gen_hand_wave) that these counters
+ * instrument; both are exact (tests/test_gpu_solver_stress.py runs the
+ * fallback), but the counters describe the fallback's work, not the shipped
+ * path's. */
 int bb_debug_counters(bb_env* env, uint64_t* h_out);
 
 /* Synthetic random policy on its own (see bb_step_out.next_action). */

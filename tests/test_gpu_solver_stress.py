@@ -47,8 +47,22 @@ def _case(rng, fill):
 @pytest.mark.parametrize("fill", [0.45, 0.6, 0.7, 0.8, 0.9, 0.95, -1.0])
 @pytest.mark.parametrize("pack", ["1,0", "32,32", "3,7"])
 def test_crowded_board_hand_generation(cuda, fill, pack, monkeypatch):
-    """pack = escalation pass schedule (first pass attempts, later passes;
-    0 = doubling): every schedule must give the same hands."""
+    """pack = escalation schedule (attempts per env in the first round, in
+    later rounds; 0 = double the previous round's, capped at 32): every
+    schedule must give the same hands."""
+    _crowded(cuda, fill, pack, monkeypatch)
+
+
+@pytest.mark.parametrize("fill", [0.6, 0.8, 0.95, -1.0])
+def test_crowded_board_debug_fallback(cuda, fill, monkeypatch):
+    """BB_DEBUG_MODE=2 (the solver counters) switches escalate_kernel to the
+    one-env-at-a-time wave search (gen_hand_wave, bbvec.h bb_debug_counters):
+    that path must stay bit-exact too."""
+    monkeypatch.setenv("BB_DEBUG_MODE", "2")
+    _crowded(cuda, fill, "8,32", monkeypatch)
+
+
+def _crowded(cuda, fill, pack, monkeypatch):
     from runtime.device_env import DeviceEnvBatch
 
     first, nxt = pack.split(",")

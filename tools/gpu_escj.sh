@@ -1,6 +1,8 @@
 #!/bin/bash
 # Escalate-kernel variants on top of the multi-env search: jump table in LDS,
 # 128-thread blocks.  Env parity + solver stress per variant, then step times.
+# Variant libraries (flags in tools/variants.py), built on the CPU beforehand:
+#   python tools/variants.py build escj escjb128 escb128
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp

@@ -2,6 +2,8 @@
 # Escalate kernel with the multi-env hand search: full -m gpu suite on the
 # default build, env parity on the group-size variants, step times per variant,
 # then the step-mode bench line.
+# Variant libraries (flags in tools/variants.py), built on the CPU beforehand:
+#   python tools/variants.py build esc0 escg16 escg32
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp

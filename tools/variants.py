@@ -28,7 +28,9 @@ VARIANTS = {
     "fair1": ["-DBB_ROLL_FAIR=1"],
     # round-1 escalate variants (their flags were not recorded)
     "esc0": ["-DBB_ESC_MULTI=0", "-DBB_ESC_GROUP=8"],
+    "escg8": ["-DBB_ESC_GROUP=8"],
     "escg16": ["-DBB_ESC_GROUP=16"],
+    "escg32": ["-DBB_ESC_GROUP=32"],  # == the shipped default, kept as a named A/B arm
     "escj": ["-DBB_ESC_LDS_JUMP=1"],
     "escjb128": ["-DBB_ESC_LDS_JUMP=1", "-DBB_ESC_BLOCK=128"],
     "escb128": ["-DBB_ESC_BLOCK=128"],
