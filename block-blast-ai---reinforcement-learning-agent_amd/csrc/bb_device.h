@@ -26,15 +26,24 @@ constexpr uint64_t kCenter = 0x00003C3C3C3C0000ull;  // rows 2-5 x cols 2-5 (boa
 //             blocked-anchor dilation is a fixed 9-step OR chain with no branch
 //   ym      : 128-bit "mirror" with bit (64 - o) for every cell offset o, the
 //             seed of the pair-conflict masks of bb_solver.h
+//   sh      : the cell offsets as a Minkowski program S = X + {0,s1} + {0,s2}
+//             with |X| <= 4 (linear offsets; built on the host and checked
+//             exact there): sh[0..3] the offsets of X (repeated to fill),
+//             sh[4] = s1, sh[5] = s2 (0 = no step) | cell count << 8.  One
+//             word per shift, so each is a 64-bit shift's amount operand as
+//             is (the hardware reads bits 5:0).  anchors_of costs 6 shifts
+//             for every piece instead of one per cell (9 for SQUARE_3x3 =
+//             {0,1,2} + {0,8} + {0,8}).
 struct PieceRow {
   uint64_t shape;
   uint64_t anchors;
   uint64_t offs;
   uint64_t ym_lo;
   uint64_t ym_hi;
-  uint32_t ncells;
-  uint32_t pad;
+  uint32_t sh[6];
 };
+
+__host__ __device__ inline uint32_t ncells_of(const PieceRow& p) { return (p.sh[5] >> 8) & 0xFFu; }
 
 // PCG64 jump-ahead table row c: A^c and S_c = sum_{i<c} A^i (mod 2^128), so
 // the state after c steps is A^c * s + inc * S_c (built on the host).
@@ -42,6 +51,21 @@ constexpr int kJumpMax = 64;
 struct JumpRow {
   uint64_t a_lo, a_hi, s_lo, s_hi;
 };
+
+// Board.can_place over all anchors at once (board.py:71-93 x engine.py:364-380):
+// anchor a is blocked iff some cell a+off is filled, i.e. bit a of (B >> off).
+// The OR over the cell offsets runs as the row's Minkowski program (PieceRow
+// sh): 4 shifts for X, then x |= x >> s for each step.  Every bit a term
+// reads at a legal anchor a is a cell of the piece placed at a, so nothing
+// wraps or leaves the board there; other anchors are masked off.
+__host__ __device__ inline uint64_t dilate(const PieceRow& p, uint64_t B) {
+  // sh[0..4] < 64 by construction (no mask needed); sh[5] carries the cell count above bit 7
+  uint64_t x = (B >> p.sh[0]) | (B >> p.sh[1]);
+  x |= (B >> p.sh[2]) | (B >> p.sh[3]);
+  x |= x >> p.sh[4];
+  x |= x >> (p.sh[5] & 63u);
+  return x;
+}
 
 // Packed hand word (also the host-visible layout, see bbvec.h bb_state_view).
 __host__ __device__ inline uint32_t hand_id(uint32_t h, int slot) { return (h >> (6 * slot)) & 63u; }
@@ -57,38 +81,28 @@ __host__ __device__ inline uint32_t hand_pack(uint32_t a, uint32_t b, uint32_t c
 // Bitboard rules
 // --------------------------------------------------------------------------
 
-// Board.can_place over all anchors at once (board.py:71-93 x engine.py:364-380):
-// anchor a is blocked iff some cell a+off is filled, i.e. bit a of (B >> off).
-__device__ __forceinline__ uint64_t anchors_of(const PieceRow& p, uint64_t B) {
-  uint64_t acc = 0;
-  uint64_t offs = p.offs;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    acc |= B >> (offs & 63u);
-    offs >>= 6;
-  }
-  return p.anchors & ~acc;
-}
+__device__ __forceinline__ uint64_t anchors_of(const PieceRow& p, uint64_t B) { return p.anchors & ~dilate(p, B); }
 
 // Board.find_complete_lines + clear_lines (board.py:144-193), and the DFS's
 // _simulate_line_clears (engine.py:226-238): full rows/cols are found on the
-// same board, then their union is cleared.
+// same board, then their union is cleared.  Worked on the two 32-bit halves
+// (rows 0-3 / 4-7): a row byte is full iff its low 7 bits carry into bit 7
+// and bit 7 is set; the columns are the AND of all eight row bytes.
+__device__ __forceinline__ uint32_t full_row_bytes(uint32_t h) {  // 0x80 in every 0xFF byte
+  return ((h & 0x7F7F7F7Fu) + 0x01010101u) & h & 0x80808080u;
+}
+
 __device__ __forceinline__ uint64_t clear_full(uint64_t B, int& rows, int& cols) {
-  uint64_t r = B & (B >> 1);
-  r &= r >> 2;
-  r &= r >> 4;
-  r &= kCol0;  // bit 8k set iff row k full
-  uint64_t c = B & (B >> 8);
-  c &= c >> 16;
-  c &= c >> 32;
-  c &= 0xFFull;  // bit k set iff column k full
-  rows = __popcll(r);
-  cols = __popcll(c);
-  uint64_t rm = (r << 8) - r;  // spread each row bit over its byte
-  uint64_t cm = c | (c << 8);
-  cm |= cm << 16;
-  cm |= cm << 32;
-  return B & ~(rm | cm);
+  const uint32_t lo = (uint32_t)B, hi = (uint32_t)(B >> 32);
+  const uint32_t flo = full_row_bytes(lo), fhi = full_row_bytes(hi);
+  uint32_t a = lo & hi;
+  a &= a >> 16;
+  a &= a >> 8;                                          // byte 0: the full columns
+  const uint32_t cs = __builtin_amdgcn_perm(a, a, 0u);  // byte 0 broadcast to all four bytes
+  rows = __popc(flo) + __popc(fhi);
+  cols = __popc(a & 0xFFu);
+  const uint32_t rlo = (flo >> 7) * 0xFFu, rhi = (fhi >> 7) * 0xFFu;  // full rows spread over their bytes
+  return ((uint64_t)(hi & ~(rhi | cs)) << 32) | (lo & ~(rlo | cs));
 }
 
 __device__ __forceinline__ uint64_t clear_full(uint64_t B) {

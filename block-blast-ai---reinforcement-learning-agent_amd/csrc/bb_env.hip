@@ -154,7 +154,7 @@ __device__ __forceinline__ bool apply_move(const Tables& t, StepCtx& s, int act)
   }
   s.valid = valid;
   if (!valid) return false;
-  s.nblk = (int)pr.ncells;
+  s.nblk = (int)ncells_of(pr);
   used |= 1u << p;
   s.moves += 1;
   s.blocks += s.nblk;

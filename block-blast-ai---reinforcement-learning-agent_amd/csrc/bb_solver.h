@@ -39,13 +39,11 @@ constexpr int kTickG = 1;
 constexpr int kTickQ = 1;
 
 __device__ __forceinline__ bool has_full_line(uint64_t B) {
-  uint64_t r = B & (B >> 1);
-  r &= r >> 2;
-  r &= r >> 4;
-  uint64_t c = B & (B >> 8);
-  c &= c >> 16;
-  c &= c >> 32;
-  return ((r & kCol0) | (c & 0xFFull)) != 0ull;
+  const uint32_t lo = (uint32_t)B, hi = (uint32_t)(B >> 32);
+  uint32_t a = lo & hi;
+  a &= a >> 16;
+  a &= a >> 8;
+  return ((full_row_bytes(lo) | full_row_bytes(hi)) | (a & 0xFFu)) != 0u;
 }
 
 // High 64 bits of a 128-bit value shifted left by s (0 <= s < 64).
@@ -59,7 +57,7 @@ __device__ __forceinline__ void pair_conflict_mask(const PieceRow& y, const Piec
   lo = 0;
   hi = 0;
   uint64_t offs = z.offs;
-  for (uint32_t j = 0; j < z.ncells; ++j) {
+  for (uint32_t j = 0, nz = ncells_of(z); j < nz; ++j) {
     const int o = (int)(offs & 63u);
     offs >>= 6;
     lo |= y.ym_lo << o;
@@ -192,18 +190,14 @@ __device__ __forceinline__ int pair_quick(uint64_t B1, const PieceRow& pb, const
 // highest anchor, then pair_quick.  True on an accept (an exact success).
 __device__ __forceinline__ bool quick_slots(uint64_t B, uint32_t x0, uint32_t x1, uint32_t x2, const PieceRow* tbl,
                                             const uint8_t* dtab, int k0, int slots) {
-  uint64_t A[3];
-  A[0] = anchors_of(tbl[x0], B);
-  A[1] = anchors_of(tbl[x1], B);
-  A[2] = anchors_of(tbl[x2], B);
 #pragma unroll
   for (int kk = 0; kk < 6; ++kk) {
     if (kk >= slots) break;
     const int k = k0 + kk;
     const int f = k % 3;
-    const uint64_t Af = f == 0 ? A[0] : (f == 1 ? A[1] : A[2]);
-    if (!Af) continue;
     const uint32_t fi = f == 0 ? x0 : (f == 1 ? x1 : x2);
+    const uint64_t Af = anchors_of(tbl[fi], B);  // only the first piece's anchors: one dilation per slot
+    if (!Af) continue;
     const uint32_t bi = f == 0 ? x1 : x0;
     const uint32_t ci = f == 2 ? x1 : x2;
     const int p = k < 3 ? __ffsll((unsigned long long)Af) - 1 : 63 - __clzll((long long)Af);
