@@ -169,6 +169,42 @@ __device__ __forceinline__ uint32_t draw_piece(Pcg& s) {
   return (uint32_t)(m >> 32);
 }
 
+// get_random_pieces(3, rng) (pieces.py:350-355): three draws without a
+// branch on has_uint32 -- the two LCG outputs the three 32-bit values can need
+// are computed unconditionally and the values picked by select, so a wave
+// with mixed has_uint32 runs two LCG steps instead of three masked ones.  A
+// Lemire rejection (p ~ 5e-9 per draw) redoes the draws sequentially.
+__device__ __forceinline__ void draw3(Pcg& s, uint32_t& a, uint32_t& b, uint32_t& c) {
+  const Pcg s0 = s;
+  const uint64_t o1 = pcg_next64(s);
+  const uint64_t h1 = s.hi, l1 = s.lo;
+  const uint64_t o2 = pcg_next64(s);
+  const bool has = s0.has != 0u;
+  const uint32_t v0 = has ? s0.buf : (uint32_t)o1;
+  const uint32_t v1 = has ? (uint32_t)o1 : (uint32_t)(o1 >> 32);
+  const uint32_t v2 = has ? (uint32_t)(o1 >> 32) : (uint32_t)o2;
+  const uint64_t m0 = (uint64_t)v0 * 37ull, m1 = (uint64_t)v1 * 37ull, m2 = (uint64_t)v2 * 37ull;
+  if ((uint32_t)m0 < 7u || (uint32_t)m1 < 7u || (uint32_t)m2 < 7u) {  // rare: numpy's rejection loop
+    s = s0;
+    a = draw_piece(s);
+    b = draw_piece(s);
+    c = draw_piece(s);
+    return;
+  }
+  a = (uint32_t)(m0 >> 32);
+  b = (uint32_t)(m1 >> 32);
+  c = (uint32_t)(m2 >> 32);
+  if (has) {  // one LCG output used, its upper half consumed (numpy keeps the stale value in `uinteger`)
+    s.hi = h1;
+    s.lo = l1;
+    s.has = 0u;
+    s.buf = (uint32_t)(o1 >> 32);
+  } else {    // two used, the upper half of the second one buffered
+    s.has = 1u;
+    s.buf = (uint32_t)(o2 >> 32);
+  }
+}
+
 // --------------------------------------------------------------------------
 // Philox4x32-10 (Random123) -- synthetic policy / sampling uniforms.
 // --------------------------------------------------------------------------

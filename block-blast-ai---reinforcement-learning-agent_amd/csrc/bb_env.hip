@@ -736,9 +736,8 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #else
         // draw attempt 1 (both halves identically); each half quick-tests its own slots
         const Pcg save = s.rng;
-        const uint32_t x0 = draw_piece(s.rng);
-        const uint32_t x1 = draw_piece(s.rng);
-        const uint32_t x2 = draw_piece(s.rng);
+        uint32_t x0, x1, x2;
+        draw3(s.rng, x0, x1, x2);
         ids = x0 | (x1 << 6) | (x2 << 12);
         park = !quick_slots(s.B, x0, x1, x2, t.row, t.d, half * BB_ROLL_KSTEP, BB_ROLL_SLOTS);
         after = s.rng;

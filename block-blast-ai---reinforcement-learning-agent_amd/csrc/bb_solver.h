@@ -216,9 +216,8 @@ __device__ __forceinline__ bool quick_slots(uint64_t B, uint32_t x0, uint32_t x1
 __device__ __forceinline__ bool quick_hand(uint64_t B, Pcg& rng, uint32_t& ids, const PieceRow* tbl,
                                            const uint8_t* dtab, int slots) {
   const Pcg save = rng;
-  const uint32_t x0 = draw_piece(rng);
-  const uint32_t x1 = draw_piece(rng);
-  const uint32_t x2 = draw_piece(rng);
+  uint32_t x0, x1, x2;
+  draw3(rng, x0, x1, x2);
   ids = x0 | (x1 << 6) | (x2 << 12);
   uint64_t A[3];
   A[0] = anchors_of(tbl[x0], B);
@@ -495,6 +494,10 @@ __device__ __forceinline__ bool slow_phase_wave(bool need, uint64_t B1, uint32_t
 //  * the batch starts at one attempt and doubles after each failed batch.
 // ---------------------------------------------------------------------------
 constexpr int kPack = 32;
+#ifndef BB_MULTI_PASSES
+#define BB_MULTI_PASSES 3  // gen_hands_multi: a round packs attempts for up to this many 64-slot passes
+#endif
+constexpr int kMultiPasses = BB_MULTI_PASSES;
 static_assert(3 * kPack / 2 + 2 <= kJumpMax, "jump table too short for the batch size");
 
 __device__ __forceinline__ void mul128(uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi, uint64_t& lo,
@@ -797,7 +800,8 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
     const uint32_t S = valid ? (uint32_t)(__popcll(eA0) + __popcll(eA1) + __popcll(eA2)) : 0u;
     const uint32_t incl = wave_incl_add(S);
     const int e_off = (int)(incl - S);
-    int nb = __popcll(__ballot(lane < nl && incl <= 64u));  // leading attempt lanes that fit one pass
+    // leading attempt lanes whose slots fit kMultiPasses passes of 64
+    int nb = __popcll(__ballot(lane < nl && incl <= 64u * kMultiPasses));
     if (nb == 0) nb = 1;
     const uint64_t packed = (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)) & __ballot(valid);
     const int total = __builtin_amdgcn_readlane((int)incl, nb - 1);
@@ -860,14 +864,24 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       // exact search only where no attempt of the same env up to this one accepted already
       const uint64_t jenv = every << (j % E);
       bool ok = q == 1;
-      const bool need = q == 2 && !(qam & jenv & ((2ull << j) - 1ull));
+      const bool need = q == 2 && !((qam | okm) & jenv & ((2ull << j) - 1ull));
       BB_MT(q1);
       if (__ballot(need)) ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds);
       BB_MT(q2);
       pq += q1 - q0;
       ps += q2 - q1;
       okm |= __ballot((__ballot(ok) & own) != 0ull);
-      if (okm) break;  // more than one pass only for a single attempt lane: decided
+      // stop once every env is decided: it has a successful attempt lane (its
+      // earlier lanes' slots came first, so they are complete and failed), or
+      // all of its packed lanes are complete
+      if (base + 64 >= total) break;
+      const uint64_t complete = __ballot(lane < nb && incl <= (uint32_t)(base + 64));
+      bool undecided = false;
+      if (lane < E) {
+        const uint64_t envl = (every << lane) & packed;
+        undecided = !(okm & envl) && (envl & ~complete) != 0ull;
+      }
+      if (!__ballot(undecided)) break;
     }
     BB_MT(p3);
     // resolve every env of the round in its own lanes

@@ -34,6 +34,10 @@ VARIANTS = {
     "escj": ["-DBB_ESC_LDS_JUMP=1"],
     "escjb128": ["-DBB_ESC_LDS_JUMP=1", "-DBB_ESC_BLOCK=128"],
     "escb128": ["-DBB_ESC_BLOCK=128"],
+    # gen_hands_multi: attempt batch sized for 1..4 passes of 64 slots (shipped 3)
+    "mp1": ["-DBB_MULTI_PASSES=1"],
+    "mp2": ["-DBB_MULTI_PASSES=2"],
+    "mp4": ["-DBB_MULTI_PASSES=4"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
     "diag3": ["-DBB_ROLL_DIAG=3"],
 }
