@@ -332,10 +332,18 @@ class PPOAgent(BaseAgent):
 
     # ------------------------------------------------------ device fast path
     def act_device(self, x: torch.Tensor, mask_bits: torch.Tensor, env_offset: int = 0,
-                   deterministic: bool = False):
-        """Rollout step on device tensors: (action int64, log-prob, value)."""
+                   deterministic: bool = False, step_base: Optional[torch.Tensor] = None, step_add: int = 0):
+        """Rollout step on device tensors: (action int64, log-prob, value).
+        With ``step_base`` (graph capture) the sampling step is
+        ``step_base[0] + step_add`` read on the device, and ``sample_step`` is
+        left to the caller (who advances both between replays)."""
         with torch.no_grad():
             logits, value = self._raw(x)
+            if step_base is not None:
+                a, lp, _ = K.masked_sample(logits, mask_bits, seed=self.sample_seed, step=step_add,
+                                           env_offset=env_offset, deterministic=deterministic, want_entropy=False,
+                                           step_base=step_base)
+                return a, lp, value
             step = self.sample_step
             self.sample_step += 1
             a, lp, _ = K.masked_sample(logits, mask_bits, seed=self.sample_seed, step=step, env_offset=env_offset,

@@ -474,9 +474,22 @@ int bb_masked_sample(const float* d_logits, const uint64_t* d_mask_bits, int32_t
                      void* stream) {
   if (!d_logits || !d_mask_bits || n < 0) return fail(nullptr, BB_ERR_ARG, "bb_masked_sample: bad arguments");
   if (n == 0) return BB_OK;
-  hipError_t st = launch_masked_sample(d_logits, d_mask_bits, n, d_uniform, seed, step, env_offset, deterministic,
+  hipError_t st = launch_masked_sample(d_logits, d_mask_bits, n, d_uniform, seed, step, nullptr, env_offset, deterministic,
                                        d_action_in, d_action, d_logp, d_entropy, (hipStream_t)stream);
   if (st != hipSuccess) return fail(nullptr, BB_ERR_HIP, std::string("bb_masked_sample: ") + hipGetErrorString(st));
+  return BB_OK;
+}
+
+int bb_masked_sample_dstep(const float* d_logits, const uint64_t* d_mask_bits, int32_t n, uint64_t seed,
+                           const uint64_t* d_step, uint64_t step_add, uint64_t env_offset, int32_t deterministic,
+                           int64_t* d_action, float* d_logp, float* d_entropy, void* stream) {
+  if (!d_logits || !d_mask_bits || !d_step || n < 0)
+    return fail(nullptr, BB_ERR_ARG, "bb_masked_sample_dstep: bad arguments");
+  if (n == 0) return BB_OK;
+  hipError_t st = launch_masked_sample(d_logits, d_mask_bits, n, nullptr, seed, step_add, d_step, env_offset,
+                                       deterministic, nullptr, d_action, d_logp, d_entropy, (hipStream_t)stream);
+  if (st != hipSuccess)
+    return fail(nullptr, BB_ERR_HIP, std::string("bb_masked_sample_dstep: ") + hipGetErrorString(st));
   return BB_OK;
 }
 

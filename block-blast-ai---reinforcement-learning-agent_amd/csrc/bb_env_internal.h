@@ -84,8 +84,9 @@ hipError_t launch_refresh_mask(const EnvDev& e, const PieceRow* rows, hipStream_
 hipError_t launch_random_actions(const uint64_t* mbits, int n, uint64_t seed, uint64_t step, uint64_t offset,
                                  int32_t* out, hipStream_t s);
 hipError_t launch_masked_sample(const float* logits, const uint64_t* mbits, int n, const float* uniform,
-                                uint64_t seed, uint64_t step, uint64_t offset, int deterministic,
-                                const int64_t* action_in, int64_t* action, float* logp, float* ent, hipStream_t s);
+                                uint64_t seed, uint64_t step, const uint64_t* d_step, uint64_t offset,
+                                int deterministic, const int64_t* action_in, int64_t* action, float* logp,
+                                float* ent, hipStream_t s);
 hipError_t launch_gae(const float* r, const float* v, const float* d, const float* last, int T, int N, float gamma,
                       float gl, float* adv, float* ret, hipStream_t s);
 

@@ -45,13 +45,15 @@ constexpr float kEps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps (cl
 __global__ void __launch_bounds__(256) masked_sample_kernel(const float* __restrict__ logits,
                                                             const uint64_t* __restrict__ mbits, int n,
                                                             const float* __restrict__ uniform, uint64_t seed,
-                                                            uint64_t step, uint64_t offset, int deterministic,
+                                                            uint64_t step, const uint64_t* __restrict__ d_step,
+                                                            uint64_t offset, int deterministic,
                                                             const int64_t* __restrict__ action_in,
                                                             int64_t* __restrict__ action_out,
                                                             float* __restrict__ logp_out, float* __restrict__ ent_out) {
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  if (d_step) step += d_step[0];  // graph replays: the base step lives in device memory
   for (int row = wave; row < n; row += nwaves) {
     float x[3];
     bool v[3];
@@ -188,14 +190,15 @@ __global__ void gae_kernel(const float* __restrict__ r, const float* __restrict_
 }
 
 hipError_t launch_masked_sample(const float* logits, const uint64_t* mbits, int n, const float* uniform,
-                                uint64_t seed, uint64_t step, uint64_t offset, int deterministic,
-                                const int64_t* action_in, int64_t* action, float* logp, float* ent, hipStream_t s) {
+                                uint64_t seed, uint64_t step, const uint64_t* d_step, uint64_t offset,
+                                int deterministic, const int64_t* action_in, int64_t* action, float* logp,
+                                float* ent, hipStream_t s) {
   int64_t waves = n;
   int64_t blocks = (waves * 64 + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(masked_sample_kernel, dim3((unsigned)blocks), dim3(256), 0, s, logits, mbits, n, uniform, seed,
-                     step, offset, deterministic, action_in, action, logp, ent);
+                     step, d_step, offset, deterministic, action_in, action, logp, ent);
   return hipGetLastError();
 }
 

@@ -47,17 +47,32 @@ def masked_sample(
     deterministic: bool = False,
     action_in: Optional[torch.Tensor] = None,
     want_entropy: bool = True,
+    step_base: Optional[torch.Tensor] = None,
 ) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
     """Fused masked softmax / Categorical / sample / log-prob / masked entropy
     (network.py:173-180, 210-262).  logits f32 (N,192) unmasked; mask_bits
-    int64 (N,3).  Returns (action int64, log_prob f32, entropy f32)."""
-    _need_cuda(logits, mask_bits, uniform, action_in)
+    int64 (N,3).  Returns (action int64, log_prob f32, entropy f32).
+    ``step_base``: an int64 device tensor of one element; the Philox step is
+    then ``step_base[0] + step``, read by the kernel (bb_masked_sample_dstep),
+    so a launch captured in a HIP graph samples afresh on every replay."""
+    _need_cuda(logits, mask_bits, uniform, action_in, step_base)
     logits = logits.contiguous().float()
     n = logits.shape[0]
     dev = logits.device
     act = torch.empty(n, dtype=torch.int64, device=dev)
     logp = torch.empty(n, dtype=torch.float32, device=dev)
     ent = torch.empty(n, dtype=torch.float32, device=dev) if want_entropy else None
+    if step_base is not None:
+        if uniform is not None or action_in is not None:
+            raise ValueError("masked_sample: step_base excludes uniform / action_in")
+        assert step_base.dtype == torch.int64 and step_base.numel() == 1
+        L.check(
+            L.load().bb_masked_sample_dstep(_p(logits), _p(mask_bits.contiguous()), n, seed, _p(step_base), step,
+                                            env_offset, int(bool(deterministic)), _p(act), _p(logp), _p(ent),
+                                            _s(dev)),
+            "bb_masked_sample_dstep",
+        )
+        return act, logp, ent
     if uniform is not None:
         uniform = uniform.contiguous().float()
     if action_in is not None:

@@ -128,6 +128,7 @@ SIGNATURES = {
     "bb_debug_counters": (C.c_int, [_P, _P]),
     "bb_random_actions": (C.c_int, [_P, _I32, _U64, _U64, _U64, _P, _P]),
     "bb_masked_sample": (C.c_int, [_P, _P, _I32, _P, _U64, _U64, _U64, _I32, _P, _P, _P, _P, _P]),
+    "bb_masked_sample_dstep": (C.c_int, [_P, _P, _I32, _U64, _P, _U64, _U64, _I32, _P, _P, _P, _P]),
     "bb_gae": (C.c_int, [_P, _P, _P, _P, _I32, _I32, _F, _F, _P, _P, _P]),
     "bb_gather_obs": (C.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P]),
     "bb_bn_workspace_bytes": (C.c_int64, [_I32, _I32, _I32, _I32, _I32]),

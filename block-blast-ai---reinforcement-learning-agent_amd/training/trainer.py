@@ -118,20 +118,51 @@ class DeviceRollout:
         # final score / moves of episodes ending at (t, i); valid where dones[t, i] == 1
         self.ep_score = torch.zeros((rollout_steps, num_envs), dtype=torch.int64, device=device)
         self.ep_moves = torch.zeros((rollout_steps, num_envs), dtype=torch.int32, device=device)
+        self._graph = None          # captured rollout (collect(graph=True))
+        self._graph_warm = False
+        self._step_base = None
 
     def reset(self) -> None:
         self.env.reset()
         self.env.obs(x=self.x, mask_bits=self.mask_bits)
 
-    def collect(self, agent: PPOAgent) -> None:
-        """scripts/train.py:173-203 for this shard, entirely on the device."""
+    def collect(self, agent: PPOAgent, graph: bool = False) -> None:
+        """scripts/train.py:173-203 for this shard, entirely on the device.
+
+        ``graph=True`` (BASELINE config 5): the T rollout steps -- snapshot,
+        CNN forward, fused masked sample, bb_step, buffer writes, observation
+        expansion -- are captured once into one HIP graph and replayed on later
+        calls (the first call runs eagerly and warms MIOpen / hipBLASLt up).
+        The sampling step comes from a device counter (bb_masked_sample_dstep)
+        so replays draw fresh uniforms; outputs equal the eager loop's for the
+        same counter value."""
+        if not graph or not self.env.device.type == "cuda":
+            self._collect_steps(agent)
+            return
+        if self._graph is None and not self._graph_warm:
+            self._collect_steps(agent)  # eager warm-up: library algorithm selection, workspaces
+            self._graph_warm = True
+            return
+        if self._graph is None:
+            self._step_base = torch.zeros(1, dtype=torch.int64, device=self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._collect_steps(agent, step_base=self._step_base)
+            self._graph = g
+        self._step_base.fill_(agent.sample_step)
+        self._graph.replay()
+        agent.sample_step += self.T
+        self.buffer.ptr, self.buffer.full = self.T, True
+
+    def _collect_steps(self, agent: PPOAgent, step_base: Optional[torch.Tensor] = None) -> None:
         buf, env = self.buffer, self.env
         buf.reset()
         info64 = env.info.view(torch.int64).view(self.n, 7)
         info32 = env.info.view(torch.int32).view(self.n, 14)
         for t in range(self.T):
             env.snapshot(board=buf.board[t], hand=buf.hand[t], mask_bits=buf.mask_bits[t])
-            a, lp, v = agent.act_device(self.x, buf.mask_bits[t], env_offset=self.offset)
+            a, lp, v = agent.act_device(self.x, buf.mask_bits[t], env_offset=self.offset, step_base=step_base,
+                                        step_add=t)
             buf.actions[t].copy_(a)
             buf.log_probs[t].copy_(lp)
             buf.values[t].copy_(v)
@@ -219,6 +250,8 @@ def train(config: Dict[str, Any], resume_path: Optional[str] = None, seed: int =
     if main:
         print(f"Created PPO agent with {sum(p.numel() for p in agent.network.parameters()):,} parameters")
     local_batch = max(1, agent_cfg.batch_size // world)
+    # BASELINE config 5: the rollout step captured in a HIP graph (training.graph_rollout)
+    graph_rollout = bool(train_cfg.get("graph_rollout", False)) and device.type == "cuda"
 
     start_step = 0
     if resume_path and os.path.exists(resume_path):
@@ -250,7 +283,7 @@ def train(config: Dict[str, Any], resume_path: Optional[str] = None, seed: int =
 
     try:
         while global_step < total_timesteps:
-            roll.collect(agent)
+            roll.collect(agent, graph=graph_rollout)
             global_step += num_envs * rollout_steps
             cnt, smax, scores, moves = roll.episodes(world)
             if cnt:

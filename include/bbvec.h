@@ -231,6 +231,18 @@ int bb_masked_sample(const float* d_logits, const uint64_t* d_mask_bits,
                      const int64_t* d_action_in, int64_t* d_action,
                      float* d_logp, float* d_entropy, void* stream);
 
+/* bb_masked_sample with the Philox step read from device memory:
+ * step = *d_step + step_add (no d_uniform, no d_action_in).  For a rollout
+ * captured in a HIP graph (scripts/train.py:173-203 replayed per update):
+ * the captured launches keep their step_add (0 .. T-1) and the caller
+ * advances *d_step by T between replays, so every replay samples with fresh
+ * uniforms, exactly as T eager calls with step = base + t would. */
+int bb_masked_sample_dstep(const float* d_logits, const uint64_t* d_mask_bits,
+                           int32_t n, uint64_t seed, const uint64_t* d_step,
+                           uint64_t step_add, uint64_t env_offset,
+                           int32_t deterministic, int64_t* d_action,
+                           float* d_logp, float* d_entropy, void* stream);
+
 /* GAE (RolloutBuffer.compute_returns_and_advantages, ppo.py:141-169) over
  * [T][N] f32 arrays, numpy-2 float32 operation order, no FMA contraction.
  * gamma and gamma_lambda are the f32 roundings of gamma and gamma*gae_lambda

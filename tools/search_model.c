@@ -67,12 +67,14 @@ static uint64_t clear_full(uint64_t B) {
 
 static int lowbit(uint64_t x) { return __builtin_ctzll(x); }
 
+static int g_noleaf = 0;  /* pass quick test without the two leaf tests */
 static int pair_quick(uint64_t B1, int b, int c, uint64_t* A2o, uint64_t* A3o) {
   uint64_t A2 = anchors_of(b, B1), A3 = anchors_of(c, B1);
   *A2o = A2, *A3o = A3;
   if (!(A2 | A3)) return 0;
   if (A2 && __builtin_popcountll(A3) > g_dtab[b][c]) return 1;
   if (A3 && __builtin_popcountll(A2) > g_dtab[b][c]) return 1;
+  if (g_noleaf) return 2;
   if (A2 && anchors_of(c, clear_full(B1 | (g_shape[b] << lowbit(A2))))) return 1;
   if (A3 && anchors_of(b, clear_full(B1 | (g_shape[c] << lowbit(A3))))) return 1;
   return 2;
@@ -268,6 +270,7 @@ int main(int argc, char** argv) {
   int epw = 32;
   if (argc > 5) g_P = atoi(argv[5]);
   if (argc > 6) epw = atoi(argv[6]);
+  if (argc > 7) g_noleaf = atoi(argv[7]);
   init_bits();
   uint64_t* seeds = malloc(sizeof(uint64_t) * n);
   for (int i = 0; i < n; ++i) seeds[i] = 42 + (uint64_t)i;
@@ -303,7 +306,11 @@ int main(int argc, char** argv) {
       Pcg64 c = g_gens[gi].pre;
       int h[3];
       draw_hand(&c, h);
-      if (quick_slot(g_gens[gi].B, h, 0) | quick_slot(g_gens[gi].B, h, 1)) continue;
+      const int nl_save = g_noleaf;
+      g_noleaf = 0;
+      const int acc = quick_slot(g_gens[gi].B, h, 0) | quick_slot(g_gens[gi].B, h, 1);
+      g_noleaf = nl_save;
+      if (acc) continue;
       grp[E++] = &g_gens[gi];
     }
     if (E) {

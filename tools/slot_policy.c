@@ -73,7 +73,14 @@ static int pair_quick(uint64_t B1, int b, int c, int mode) {
   if (!(A2 | A3)) return 0;
   if (A2 && __builtin_popcountll(A3) > g_dtab[b][c]) return 1;
   if (A3 && __builtin_popcountll(A2) > g_dtab[b][c]) return 1;
+  if (mode == -1) return 2;
+  if (mode == -3) {  /* leaves as "z fits on B1 | y@q" (no clear): A_z & ~conflict */
+    if (A2 && anchors_of(c, B1 | (g_shape[b] << lowbit(A2)))) return 1;
+    if (A3 && anchors_of(b, B1 | (g_shape[c] << lowbit(A3)))) return 1;
+    return 2;
+  }
   if (A2 && anchors_of(c, clear_full(B1 | (g_shape[b] << lowbit(A2))))) return 1;
+  if (mode == -2) return 2;
   if (A3 && anchors_of(b, clear_full(B1 | (g_shape[c] << lowbit(A3))))) return 1;
   if (mode >= 1) {
     if (A2 && anchors_of(c, clear_full(B1 | (g_shape[b] << highbit(A2))))) return 1;
@@ -106,7 +113,7 @@ static void order_by_anchors(uint64_t B, const int h[3], int ord[3], int* nz) {
   for (int i = 0; i < 3; ++i) { ord[i] = o2[i]; if (cnt[o2[i]]) (*nz)++; }
 }
 
-enum { NPOL = 12 };
+enum { NPOL = 15 };
 static const char* pol_names[NPOL] = {
   "shipped: f0 low | f1 low",
   "f0 low | f0 high",
@@ -120,6 +127,9 @@ static const char* pol_names[NPOL] = {
   "least low|high, 2nd low|high (4 slots)",
   "f0 low | f1 high",
   "least low | 2nd least high",
+  "shipped slots, |D| bound only",
+  "shipped slots, |D| + first order leaf",
+  "shipped slots, leaves without clears",
 };
 static uint64_t acc_cnt[NPOL], n_first, n_ok;
 
@@ -145,6 +155,9 @@ static void gen_hook(const struct Engine* ee, int attempt, int ok) {
   r[9] = r[4] | slot_test(B, h, ord[1], 0, 0) | slot_test(B, h, ord[1], 1, 0);
   r[10] = slot_test(B, h, 0, 0, 0) | slot_test(B, h, 1, 1, 0);
   r[11] = slot_test(B, h, ord[0], 0, 0) | slot_test(B, h, ord[1], 1, 0);
+  r[12] = slot_test(B, h, 0, 0, -1) | slot_test(B, h, 1, 0, -1);
+  r[13] = slot_test(B, h, 0, 0, -2) | slot_test(B, h, 1, 0, -2);
+  r[14] = slot_test(B, h, 0, 0, -3) | slot_test(B, h, 1, 0, -3);
   for (int k = 0; k < NPOL; ++k) {
     if (r[k] && !ok) { fprintf(stderr, "UNSOUND %d\n", k); exit(1); }
     acc_cnt[k] += r[k];

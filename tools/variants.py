@@ -40,6 +40,10 @@ VARIANTS = {
     "mp4": ["-DBB_MULTI_PASSES=4"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
     "diag3": ["-DBB_ROLL_DIAG=3"],
+    # NOT reference semantics (instruction-count attribution only): 1 = in-lane quick test, no wave
+    # search (an unaccepted draw is kept); 2 = first draw kept, no test at all
+    "diag1": ["-DBB_ROLL_DIAG=1"],
+    "diag2": ["-DBB_ROLL_DIAG=2"],
 }
 
 
