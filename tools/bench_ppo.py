@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--layout", choices=["default", "nchw", "channels_last"], default="default",
                     help="conv-stack activation layout (default: the agent's own choice)")
     ap.add_argument("--no-graph", action="store_true", help="issue the update step kernel by kernel")
+    ap.add_argument("--graph-rollout", action="store_true",
+                    help="BASELINE config 5: the rollout's T steps captured in one HIP graph and replayed")
     args = ap.parse_args()
 
     from agents import PPOAgent, PPOConfig
@@ -62,8 +64,12 @@ def main():
     agent.values_device(roll.x)
     torch.cuda.synchronize()
 
+    if args.graph_rollout:  # eager warm-up, then capture (+ one replay), all untimed
+        roll.collect(agent, graph=True)
+        roll.collect(agent, graph=True)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
-    roll.collect(agent)
+    roll.collect(agent, graph=args.graph_rollout)
     last = agent.values_device(roll.x)
     torch.cuda.synchronize()
     t_roll = time.perf_counter() - t0
@@ -90,7 +96,7 @@ def main():
     upd_flops = 3 * FWD_FLOP * args.batch / t_upd_step
     print(json.dumps({
         "workload": "BASELINE config 3: full PPO iteration on 1 MI355X", "envs": args.envs, "rollout_steps": args.rollout,
-        "miopen_find": args.miopen_find, "channels_last": agent.channels_last,
+        "miopen_find": args.miopen_find, "channels_last": agent.channels_last, "graph_rollout": args.graph_rollout,
         "batch": args.batch, "epochs": args.epochs, "compute_dtype": "bf16 autocast" if args.autocast == "bf16" else "fp32",
         "rollout_s": round(t_roll, 4), "rollout_env_steps_per_s": round(samples / t_roll, 1),
         "rollout_cnn_tflops": round(roll_flops / 1e12, 2),
