@@ -593,8 +593,9 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
 #ifndef BB_ROLL_ENVS
 #define BB_ROLL_ENVS 32
 #endif
-constexpr int kRollEnvs = BB_ROLL_ENVS;  // 32 (two copies per env) or 16 (four)
-static_assert(kRollEnvs == 16 || kRollEnvs == 32, "envs per wave");
+constexpr int kRollEnvs = BB_ROLL_ENVS;  // 32 (two copies per env), 16 (four) or 64 (one: 1 wave per SIMD)
+static_assert(kRollEnvs == 16 || kRollEnvs == 32 || kRollEnvs == 64, "envs per wave");
+constexpr uint64_t kRollEnvMask = kRollEnvs >= 64 ? ~0ull : ((1ull << (kRollEnvs & 63)) - 1ull);
 #ifndef BB_ROLL_BLOCK
 #define BB_ROLL_BLOCK 512  // 8 waves: at 65,536 envs one workgroup per CU, both waves of a SIMD in it
 #endif
@@ -748,7 +749,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     }
     // accept if either copy accepted; else roll back for the wave search
     uint64_t acc = ~__ballot(park) & __ballot(live && s.drew);
-    acc |= (acc >> kRollEnvs) | (acc << (64 - kRollEnvs));  // rotate: every copy sees the others
+    if (kRollEnvs < 64) acc |= (acc >> (kRollEnvs & 63)) | (acc << ((64 - kRollEnvs) & 63));  // every copy sees the others
     if (kRollEnvs == 16) acc |= (acc >> 32) | (acc << 32);
     const bool accepted = (acc >> lane) & 1ull;
     if (live && s.drew) {
@@ -759,7 +760,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       s.hand = (s.hand & 0x3FFFFu) | ((uint32_t)s.rng.has << 22);
     }
     // hand searches the in-lane test left open: the whole wave, one env at a time
-    uint64_t parked = __ballot(park) & ((1ull << kRollEnvs) - 1ull);
+    uint64_t parked = __ballot(park) & kRollEnvMask;
     BB_DIAG_T(c1);
 #if BB_MULTI
     if (parked) {

@@ -185,6 +185,29 @@ __device__ __forceinline__ int pair_quick(uint64_t B1, const PieceRow& pb, const
   return 2;
 }
 
+// pair_quick for the wave searches' passes: the two leaves test the second
+// piece on B1 | first piece WITHOUT the line clear.  Clearing only frees
+// cells, so a fit there is a fit after the clear: every accept is still an
+// exact success; the rarer accepts that need the clear are left (2) to the
+// exact phase (slow_phase_wave).  Saves the two clear_full of pair_quick.
+__device__ __forceinline__ int pair_quick_nc(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint32_t dbc,
+                                             uint64_t& A2, uint64_t& A3) {
+  A2 = anchors_of(pb, B1);
+  A3 = anchors_of(pc, B1);
+  if ((A2 | A3) == 0) return 0;
+  if (A2 && (uint32_t)__popcll(A3) > dbc) return 1;
+  if (A3 && (uint32_t)__popcll(A2) > dbc) return 1;
+  if (A2) {
+    const int q = __ffsll((unsigned long long)A2) - 1;
+    if (anchors_of(pc, B1 | (pb.shape << q))) return 1;
+  }
+  if (A3) {
+    const int r = __ffsll((unsigned long long)A3) - 1;
+    if (anchors_of(pb, B1 | (pc.shape << r))) return 1;
+  }
+  return 2;
+}
+
 // Quick test of fixed level-1 slots k0 .. k0+slots-1 of the drawn hand
 // (x0, x1, x2) on B: slot k places piece k mod 3 at its lowest (k < 3) or
 // highest anchor, then pair_quick.  True on an accept (an exact success).
@@ -498,6 +521,9 @@ constexpr int kPack = 32;
 #define BB_MULTI_PASSES 3  // gen_hands_multi: a round packs attempts for up to this many 64-slot passes
 #endif
 constexpr int kMultiPasses = BB_MULTI_PASSES;
+#ifndef BB_PASS_NC
+#define BB_PASS_NC 0  // 1: pass leaf tests without the line clear (pair_quick_nc; measured slower: more exact-phase work)
+#endif
 static_assert(3 * kPack / 2 + 2 <= kJumpMax, "jump table too short for the batch size");
 
 __device__ __forceinline__ void mul128(uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi, uint64_t& lo,
@@ -852,7 +878,11 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
         bi = hand_id(jid, f == 0 ? 1 : 0);
         ci = hand_id(jid, f == 2 ? 1 : 2);
         B1 = clear_full(jB | (tbl[hand_id(jid, f)].shape << p));
+#if BB_PASS_NC
+        q = pair_quick_nc(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
+#else
         q = pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
+#endif
       }
       // attempt lanes with a quick accept: attempt lane L owns the pass's slot
       // bits [lo, hi) of any slot ballot
@@ -917,7 +947,7 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
         }
       }
     }
-    todo &= ~(__ballot(done && lane < kEnvs) & ((1ull << kEnvs) - 1ull));
+    todo &= ~(__ballot(done && lane < kEnvs) & (kEnvs >= 64 ? ~0ull : ((1ull << (kEnvs & 63)) - 1ull)));
     pk = pack_next > 0 ? pack_next : 2 * pk;
     pk = pk < kPack ? pk : kPack;
     if (prof) {

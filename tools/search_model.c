@@ -74,7 +74,19 @@ static int pair_quick(uint64_t B1, int b, int c, uint64_t* A2o, uint64_t* A3o) {
   if (!(A2 | A3)) return 0;
   if (A2 && __builtin_popcountll(A3) > g_dtab[b][c]) return 1;
   if (A3 && __builtin_popcountll(A2) > g_dtab[b][c]) return 1;
-  if (g_noleaf) return 2;
+  if (g_noleaf == 1) return 2;
+  if (g_noleaf == 3) {  /* 4 leaves: lowest and highest anchor of each order */
+    if (A2 && anchors_of(c, clear_full(B1 | (g_shape[b] << lowbit(A2))))) return 1;
+    if (A3 && anchors_of(b, clear_full(B1 | (g_shape[c] << lowbit(A3))))) return 1;
+    if (A2 && anchors_of(c, clear_full(B1 | (g_shape[b] << (63 - __builtin_clzll(A2)))))) return 1;
+    if (A3 && anchors_of(b, clear_full(B1 | (g_shape[c] << (63 - __builtin_clzll(A3)))))) return 1;
+    return 2;
+  }
+  if (g_noleaf == 2) {  /* sound clear-free leaves: "z fits on B1 | y@q" */
+    if (A2 && anchors_of(c, B1 | (g_shape[b] << lowbit(A2)))) return 1;
+    if (A3 && anchors_of(b, B1 | (g_shape[c] << lowbit(A3)))) return 1;
+    return 2;
+  }
   if (A2 && anchors_of(c, clear_full(B1 | (g_shape[b] << lowbit(A2))))) return 1;
   if (A3 && anchors_of(b, clear_full(B1 | (g_shape[c] << lowbit(A3))))) return 1;
   return 2;
@@ -133,7 +145,8 @@ typedef struct {
   double calls, rounds, passes, slots, slow_rounds, slow_tasks, lanes_drawn, lanes_packed, envs;
 } Stats;
 
-static int g_P = 1;  /* passes (64 slots each) an attempt batch may span */
+static int g_P = 1;
+static double g_cls[2][2], g_cls_n[2][2];  /* slow tasks by slot class: [one-sided][line reachable] */  /* passes (64 slots each) an attempt batch may span */
 
 static void model_call(Gen** par, int E0, int pack_first, int pack_next, Stats* st) {
   int att[64];
@@ -204,7 +217,25 @@ static void model_call(Gen** par, int E0, int pack_first, int pack_next, Stats* 
         int blocked = 0;  /* an attempt lane of the same env up to L has succeeded */
         for (int j = L % E; j <= L; j += E) blocked |= ok_lane[j];
         if (q[x - base] == 2 && !blocked) {
-          tasks += __builtin_popcountll(A2s[x - base]) + __builtin_popcountll(A3s[x - base]);
+          const int t2 = __builtin_popcountll(A2s[x - base]) + __builtin_popcountll(A3s[x - base]);
+          tasks += t2;
+          {
+            const uint64_t a2 = A2s[x - base], a3 = A3s[x - base];
+            const int fl = slot_f[x], bb = fl == 0 ? 1 : 0, cc = fl == 2 ? 1 : 2;
+            const uint64_t B1x = clear_full(par[idx[L % E]]->B | (g_shape[hands[L][fl]] << slot_p[x]));
+            int cls = (a2 && a3) ? 0 : 1;
+            /* one-sided: only the piece with anchors can go first, and it must complete a line */
+            int reach = 1;
+            if (cls) {
+              const int y = a2 ? hands[L][bb] : hands[L][cc];
+              int r2 = 0;
+              for (int r = 0; r < 8; ++r) if (8 - __builtin_popcountll((B1x >> (8 * r)) & 0xFF) <= g_pieces[y].w) r2 = 1;
+              for (int c = 0; c < 8; ++c) if (8 - __builtin_popcountll(B1x & (0x0101010101010101ull << c)) <= g_pieces[y].h) r2 = 1;
+              reach = r2;
+            }
+            g_cls[cls][reach] += t2;
+            g_cls_n[cls][reach] += 1;
+          }
           const int f = slot_f[x], b = f == 0 ? 1 : 0, c = f == 2 ? 1 : 2;
           const uint64_t B1 = clear_full(par[idx[L % E]]->B | (g_shape[hands[L][f]] << slot_p[x]));
           if (pair_exact(B1, hands[L][b], hands[L][c])) ok_lane[L] = 1;
@@ -330,6 +361,8 @@ int main(int argc, char** argv) {
   printf("per wave-step: rounds %.3f passes %.3f slow rounds %.3f  -> modelled search %.2fk cycles\n",
          st.rounds / wave_steps, st.passes / wave_steps, st.slow_rounds / wave_steps,
          (cr * st.rounds + cp * st.passes + cs * st.slow_rounds) / wave_steps);
+  printf("slow tasks by slot class: both-sided %.0f (%.0f slots), one-sided reachable %.0f (%.0f), one-sided unreachable %.0f (%.0f)\n",
+         g_cls[0][1], g_cls_n[0][1], g_cls[1][1], g_cls_n[1][1], g_cls[1][0], g_cls_n[1][0]);
   printf("per env-step: modelled search %.1f cycles\n", (cr * st.rounds + cp * st.passes + cs * st.slow_rounds) * 1000 / wave_steps / epw);
   return 0;
 }

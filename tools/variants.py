@@ -23,6 +23,9 @@ VARIANTS = {
     # rollout kernel workgroup shape (waves per workgroup; SIMD partners share LDS progress words at 512)
     "rblk64": ["-DBB_ROLL_BLOCK=64"],
     "rblk256": ["-DBB_ROLL_BLOCK=256"],
+    # 64 envs per wave, one wave per SIMD (256-thread workgroups, no partner priority), in-lane slots 0|1
+    "e64": ["-DBB_ROLL_ENVS=64", "-DBB_ROLL_BLOCK=256", "-DBB_ROLL_FAIR=0", "-DBB_ROLL_SLOTS=2"],
+    "e64s1": ["-DBB_ROLL_ENVS=64", "-DBB_ROLL_BLOCK=256", "-DBB_ROLL_FAIR=0", "-DBB_ROLL_SLOTS=1"],
     # rollout SIMD-partner priority: 0 none, 1 alternate per step, 2 the wave behind takes it (shipped)
     "fair0": ["-DBB_ROLL_FAIR=0"],
     "fair1": ["-DBB_ROLL_FAIR=1"],
@@ -38,6 +41,8 @@ VARIANTS = {
     "mp1": ["-DBB_MULTI_PASSES=1"],
     "mp2": ["-DBB_MULTI_PASSES=2"],
     "mp4": ["-DBB_MULTI_PASSES=4"],
+    # pass leaf tests without the line clear (pair_quick_nc): measured -1.3%, not shipped
+    "passnc": ["-DBB_PASS_NC=1"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
     "diag3": ["-DBB_ROLL_DIAG=3"],
     # NOT reference semantics (instruction-count attribution only): 1 = in-lane quick test, no wave
