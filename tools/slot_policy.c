@@ -113,7 +113,7 @@ static void order_by_anchors(uint64_t B, const int h[3], int ord[3], int* nz) {
   for (int i = 0; i < 3; ++i) { ord[i] = o2[i]; if (cnt[o2[i]]) (*nz)++; }
 }
 
-enum { NPOL = 15 };
+enum { NPOL = 17 };
 static const char* pol_names[NPOL] = {
   "shipped: f0 low | f1 low",
   "f0 low | f0 high",
@@ -130,6 +130,8 @@ static const char* pol_names[NPOL] = {
   "shipped slots, |D| bound only",
   "shipped slots, |D| + first order leaf",
   "shipped slots, leaves without clears",
+  "most cells low | 2nd most cells low",
+  "most cells low | most cells high",
 };
 static uint64_t acc_cnt[NPOL], n_first, n_ok;
 
@@ -158,6 +160,14 @@ static void gen_hook(const struct Engine* ee, int attempt, int ok) {
   r[12] = slot_test(B, h, 0, 0, -1) | slot_test(B, h, 1, 0, -1);
   r[13] = slot_test(B, h, 0, 0, -2) | slot_test(B, h, 1, 0, -2);
   r[14] = slot_test(B, h, 0, 0, -3) | slot_test(B, h, 1, 0, -3);
+  {
+    int oc[3] = {0, 1, 2};
+    for (int i = 0; i < 3; ++i)
+      for (int j = i + 1; j < 3; ++j)
+        if (g_pieces[h[oc[j]]].n > g_pieces[h[oc[i]]].n) { int t = oc[i]; oc[i] = oc[j]; oc[j] = t; }
+    r[15] = slot_test(B, h, oc[0], 0, 0) | slot_test(B, h, oc[1], 0, 0);
+    r[16] = slot_test(B, h, oc[0], 0, 0) | slot_test(B, h, oc[0], 1, 0);
+  }
   for (int k = 0; k < NPOL; ++k) {
     if (r[k] && !ok) { fprintf(stderr, "UNSOUND %d\n", k); exit(1); }
     acc_cnt[k] += r[k];
