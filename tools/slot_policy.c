@@ -134,6 +134,23 @@ static const char* pol_names[NPOL] = {
   "most cells low | most cells high",
 };
 static uint64_t acc_cnt[NPOL], n_first, n_ok;
+enum { KMAX = 16 };
+static uint64_t acc_k_fixed[KMAX + 1], acc_k_dfs[KMAX + 1], acc_k_rr[KMAX + 1];
+
+/* k-th anchor (rank) of A from the low end, or from the high end when neg */
+static int rank_bit(uint64_t A, int r, int high) {
+  for (int i = 0; i < r; ++i) {
+    if (!A) return -1;
+    if (high) A &= ~(1ull << (63 - __builtin_clzll(A))); else A &= A - 1;
+  }
+  if (!A) return -1;
+  return high ? 63 - __builtin_clzll(A) : lowbit(A);
+}
+
+static int slot_at(uint64_t B, const int h[3], int f, int p) {
+  int b = f == 0 ? 1 : 0, c = f == 2 ? 1 : 2;
+  return pair_quick(clear_full(B | (g_shape[h[f]] << p)), h[b], h[c], 0) == 1;
+}
 
 static void gen_hook(const struct Engine* ee, int attempt, int ok) {
   const Engine* e = (const Engine*)ee;
@@ -168,6 +185,40 @@ static void gen_hook(const struct Engine* ee, int attempt, int ok) {
     r[15] = slot_test(B, h, oc[0], 0, 0) | slot_test(B, h, oc[1], 0, 0);
     r[16] = slot_test(B, h, oc[0], 0, 0) | slot_test(B, h, oc[0], 1, 0);
   }
+  {
+    /* fixed list: round j covers (f0,f1,f2) at the j/2-th anchor from the low (even j) or high (odd j) end */
+    uint64_t A[3] = {anchors_of(h[0], B), anchors_of(h[1], B), anchors_of(h[2], B)};
+    int hit = 0;
+    for (int k = 0; k < KMAX; ++k) {
+      const int f = k % 3, round = k / 3, high = round & 1, rank = round / 2;
+      const int p = rank_bit(A[f], rank, high);
+      if (p >= 0 && slot_at(B, h, f, p)) hit = 1;
+      acc_k_fixed[k + 1] += hit;
+    }
+    /* DFS order: f-major, anchors ascending */
+    hit = 0;
+    int k = 0;
+    for (int f = 0; f < 3 && k < KMAX; ++f)
+      for (uint64_t it = A[f]; it && k < KMAX; it &= it - 1, ++k) {
+        if (slot_at(B, h, f, lowbit(it))) hit = 1;
+        acc_k_dfs[k + 1] += hit;
+      }
+    for (; k < KMAX; ++k) acc_k_dfs[k + 1] += hit;
+    /* round-robin over f, anchors ascending within f */
+    hit = 0;
+    k = 0;
+    uint64_t it[3] = {A[0], A[1], A[2]};
+    while (k < KMAX && (it[0] | it[1] | it[2])) {
+      for (int f = 0; f < 3 && k < KMAX; ++f) {
+        if (!it[f]) continue;
+        const int p = lowbit(it[f]);
+        it[f] &= it[f] - 1;
+        if (slot_at(B, h, f, p)) hit = 1;
+        acc_k_rr[++k] += hit;
+      }
+    }
+    for (; k < KMAX; ++k) acc_k_rr[k + 1] += hit;
+  }
   for (int k = 0; k < NPOL; ++k) {
     if (r[k] && !ok) { fprintf(stderr, "UNSOUND %d\n", k); exit(1); }
     acc_cnt[k] += r[k];
@@ -191,5 +242,9 @@ int main(int argc, char** argv) {
   for (int k = 0; k < NPOL; ++k)
     printf("%-45s accept %.4f  park %.4f\n", pol_names[k], (double)acc_cnt[k] / n_first,
            1.0 - (double)acc_cnt[k] / n_first);
+  printf("k slots per drawing env:  fixed(f-rotating, low/high)  DFS(f-major)  round-robin\n");
+  for (int k = 1; k <= KMAX; ++k)
+    printf("  k=%2d  accept %.4f  %.4f  %.4f\n", k, (double)acc_k_fixed[k] / n_first, (double)acc_k_dfs[k] / n_first,
+           (double)acc_k_rr[k] / n_first);
   return 0;
 }
