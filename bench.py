@@ -8,8 +8,9 @@ kernel).  A bench "step" is one pass of the hot path over one batch:
   --mode rollout (default): one bb_rollout launch = T = 128 env-steps (the
       reference's PPO horizon, scripts/train.py:173-203 / config n_steps) of
       every env, the env state held in registers between its T steps;
-  --mode step: one bb_step launch (step + escalate kernels) = one env-step of
-      every env, the drop-in path under VectorizedBlockBlastEnv.step.
+  --mode step: one bb_step call = one env-step of every env, the drop-in path
+      under VectorizedBlockBlastEnv.step (one launch of the rollout kernel at
+      T = 1; BB_STEP_KERNELS=2 selects the step + escalate kernel pair).
 Both produce identical trajectories (tests/test_gpu_rollout.py).  `value`
 counts env-steps (envs x T x K in rollout mode, envs x K in step mode) over
 the timed wall time.
@@ -247,7 +248,9 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "kernel": ("bb_step = bb::step_kernel + bb::escalate_kernel" if args.mode == "step" else
+                "kernel": (("bb_step = bb::step_kernel + bb::escalate_kernel (BB_STEP_KERNELS=2)"
+                            if os.environ.get("BB_STEP_KERNELS") == "2" else
+                            "bb_step = one bb::rollout_kernel<true> launch at T = 1") if args.mode == "step" else
                            f"bb_rollout = bb::rollout_kernel, {T} env-steps of every env per launch"),
                 "env_steps_per_launch": n * per_launch,
                 "kernel_avg_ms": round(kern_ms, 5),

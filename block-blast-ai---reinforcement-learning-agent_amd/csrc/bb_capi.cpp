@@ -36,6 +36,9 @@ struct bb_env {
   // half-applied state) that escalate_kernel never finished; only a full
   // bb_reset (which clears every pend flag) makes the handle usable again
   bool broken = false;
+  // bb_step through the rollout kernel (T = 1) instead of step + escalate kernels; the latter serves the
+  // diagnostic modes (BB_DEBUG_MODE, BB_LANE_BUDGET, BB_LANE_QUICK) and BB_STEP_KERNELS=2
+  bool fused_step = true;
   std::string err;
 };
 
@@ -159,6 +162,8 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   if (getenv("BB_LANE_BUDGET") && !getenv("BB_LANE_QUICK")) e->lane_quick = 0;  // explicit budget mode
   if (const char* s = getenv("BB_PACK_FIRST")) e->pack_first = atoi(s) > 0 ? atoi(s) : 1;
   if (const char* s = getenv("BB_PACK_NEXT")) e->pack_next = atoi(s) > 0 ? atoi(s) : 0;
+  if (e->dbg || getenv("BB_LANE_BUDGET") || getenv("BB_LANE_QUICK")) e->fused_step = false;
+  if (const char* s = getenv("BB_STEP_KERNELS")) e->fused_step = atoi(s) != 2;
   const size_t bytes = slab_bytes(num_envs);
   st = hipMalloc(&e->slab, bytes);
   if (st != hipSuccess) {
@@ -293,7 +298,25 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.env_offset = out->env_offset;
   DeviceGuard g(env->device);
   if (env->broken) return broken_fail(env, "bb_step");
-  hipError_t st = launch_step(env->d, env->d_rows, env->d_dtab, d_actions, a, (hipStream_t)stream);
+  hipError_t st;
+  if (env->fused_step) {
+    // one launch: the rollout kernel at T = 1 (2 lanes per env, hand searches in the wave); output for
+    // output equal to the two-kernel path below (tests/test_gpu_env_parity.py runs both)
+    RollArgs r{};
+    r.steps = 1;
+    r.first_action = d_actions;
+    r.reward = out->reward;
+    r.terminated = out->terminated;
+    r.lines = out->lines;
+    r.mask = out->mask;
+    r.next_action = out->next_action;
+    r.policy_step0 = out->policy_step - 1;  // step 0's next action uses policy_step0 + 1
+    r.info = out->info;
+    r.reward_f64 = out->reward_f64;
+    st = launch_rollout(env->d, env->d_rows, env->d_dtab, a, r, (hipStream_t)stream);
+  } else {
+    st = launch_step(env->d, env->d_rows, env->d_dtab, d_actions, a, (hipStream_t)stream);
+  }
   if (st != hipSuccess) {
     env->broken = true;
     return hip_fail(env, st, "bb_step");

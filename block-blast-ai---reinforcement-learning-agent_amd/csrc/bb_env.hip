@@ -616,6 +616,9 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 #define BB_ROLL_KSTEP BB_ROLL_SLOTS  // copy c tests slots c * KSTEP, c * KSTEP + 1, ...
 #endif
 
+// kStepOut: the bb_step outputs (info record, fp64 reward) are written too --
+// the instantiation bb_step uses at T = 1; the rollout path runs without them.
+template <bool kStepOut>
 __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a, RollArgs r) {
   __shared__ Tables t;
@@ -813,13 +816,16 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       masks_of(t, s.B, s.hand, m);
       double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
       bool term = false;
+      int holes = 0;
       if (s.valid) {
         const bool over = (m[0] | m[1] | m[2]) == 0ull;  // engine.py:440-441
         if (over) s.hand |= 1u << 21;
-        int holes, center;
+        int center;
         rew = move_reward(s, a, over, holes, center);
         s.prev = (uint32_t)(holes | (center << 8));
         term = over;
+      } else if (kStepOut && r.info) {
+        holes = count_holes(s.B);
       }
       const size_t o = (size_t)step * N + (size_t)i;
       if (primary) {
@@ -827,6 +833,26 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         r.terminated[o] = term ? 1 : 0;
         if (r.lines) r.lines[o] = (uint8_t)s.lines;
         if (r.actions) r.actions[o] = act;
+        if (kStepOut && r.reward_f64) r.reward_f64[o] = rew;
+        if (kStepOut && r.info) {  // block_blast_env.py:266-288, values after the move, before the auto-reset
+          bb_info inf;
+          inf.score = s.score;
+          inf.score_gained = s.gained;
+          inf.term_board = s.B;
+          inf.moves = s.moves;
+          inf.lines = s.lines_tot;
+          inf.max_combo = s.max_combo;
+          inf.blocks = s.blocks;
+          inf.term_hand = s.hand;
+          inf.holes = (uint8_t)holes;
+          inf.filled = (uint8_t)__popcll(s.B);
+          inf.flags = (uint8_t)((s.valid ? 4u : 1u) | (term ? 2u : 0u));
+          inf.last_blocks = (uint8_t)s.nblk;
+          inf.last_lines = (uint8_t)s.lines;
+          inf.last_cm = (uint8_t)s.cm;
+          inf.pad[0] = inf.pad[1] = 0;
+          r.info[o] = inf;
+        }
       }
       if (term && a.autoreset) {  // wrappers.py:97-102
         if (s.has_seed) {
@@ -1008,7 +1034,10 @@ hipError_t launch_rollout(const EnvDev& e, const PieceRow* rows, const uint8_t* 
                           const RollArgs& r, hipStream_t s) {
   const int64_t waves = ((int64_t)e.n + kRollEnvs - 1) / kRollEnvs;
   const int64_t blocks = (waves * 64 + kRollBlock - 1) / kRollBlock;
-  hipLaunchKernelGGL(rollout_kernel, dim3((unsigned)blocks), dim3(kRollBlock), 0, s, e, rows, d, a, r);
+  if (r.info || r.reward_f64)
+    hipLaunchKernelGGL(rollout_kernel<true>, dim3((unsigned)blocks), dim3(kRollBlock), 0, s, e, rows, d, a, r);
+  else
+    hipLaunchKernelGGL(rollout_kernel<false>, dim3((unsigned)blocks), dim3(kRollBlock), 0, s, e, rows, d, a, r);
   return hipGetLastError();
 }
 

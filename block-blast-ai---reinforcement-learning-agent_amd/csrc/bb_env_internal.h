@@ -71,6 +71,8 @@ struct RollArgs {
   uint64_t* mask;               // [T][N][3] optional: post-step mask bits
   int32_t* next_action;         // [N] optional: policy action after the last step
   uint64_t policy_step0;        // step t's next action uses policy_step0 + t + 1
+  bb_info* info;                // [T][N] optional: bb_step's info record (bb_step through this kernel, T = 1)
+  double* reward_f64;           // [T][N] optional: the fp64 reward
 };
 
 hipError_t launch_reset(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const uint8_t* sel, hipStream_t s);

@@ -1,6 +1,8 @@
 """GPU parity: the gfx950 vec-env (through the C-ABI) vs the CPU oracle.
 
-Bit-exact on every step: observations (board / piece planes / int8 mask),
+Bit-exact on every step, on both bb_step paths (BB_STEP_KERNELS=1: one launch
+of the rollout kernel at T = 1, the default; 2: step_kernel + escalate_kernel):
+observations (board / piece planes / int8 mask),
 f32 rewards, terminated flags, info dicts (incl. last_move, terminal
 observation, final_score) and the full packed state.  Actions mix legal moves
 with illegal ones (used slot, collision, off-board, out-of-range ints) so the
@@ -70,12 +72,16 @@ def _run_parity(n, steps, seed, p_invalid, reward_config=None, act_seed=0):
     return terms
 
 
-def test_vec_env_bit_exact_default_rewards(cuda):
+@pytest.mark.parametrize("kernels", ["1", "2"])
+def test_vec_env_bit_exact_default_rewards(cuda, kernels, monkeypatch):
+    monkeypatch.setenv("BB_STEP_KERNELS", kernels)  # 1: fused (rollout kernel, T = 1); 2: step + escalate
     terms = _run_parity(n=96, steps=160, seed=42, p_invalid=0.1)
     assert terms > 50  # auto-reset path exercised many times
 
 
-def test_vec_env_bit_exact_custom_rewards(cuda):
+@pytest.mark.parametrize("kernels", ["1", "2"])
+def test_vec_env_bit_exact_custom_rewards(cuda, kernels, monkeypatch):
+    monkeypatch.setenv("BB_STEP_KERNELS", kernels)  # 1: fused (rollout kernel, T = 1); 2: step + escalate
     rc = {"line_clear_base": 100.0, "block_placed": 1.0, "game_over_penalty": -500.0, "hole_penalty": -0.3,
           "center_bonus": 0.7, "combo_multiplier_bonus": 3.25}
     _run_parity(n=64, steps=120, seed=7, p_invalid=0.05, reward_config=rc, act_seed=3)
@@ -95,11 +101,15 @@ def test_vec_env_solver_paths(cuda, monkeypatch, budget):
     assert terms > 20
 
 
-def test_vec_env_all_invalid_and_edge_actions(cuda):
+@pytest.mark.parametrize("kernels", ["1", "2"])
+def test_vec_env_all_invalid_and_edge_actions(cuda, kernels, monkeypatch):
+    monkeypatch.setenv("BB_STEP_KERNELS", kernels)  # 1: fused (rollout kernel, T = 1); 2: step + escalate
     _run_parity(n=16, steps=20, seed=123, p_invalid=1.0, act_seed=5)
 
 
-def test_vec_env_reset_with_new_seed(cuda):
+@pytest.mark.parametrize("kernels", ["1", "2"])
+def test_vec_env_reset_with_new_seed(cuda, kernels, monkeypatch):
+    monkeypatch.setenv("BB_STEP_KERNELS", kernels)  # 1: fused (rollout kernel, T = 1); 2: step + escalate
     from environment.wrappers import VectorizedBlockBlastEnv
 
     gpu = VectorizedBlockBlastEnv(8, seed=1, device="cuda:0")
@@ -123,7 +133,9 @@ def test_vec_env_reset_with_new_seed(cuda):
     gpu.close()
 
 
-def test_fused_random_policy_matches_oracle(cuda):
+@pytest.mark.parametrize("kernels", ["1", "2"])
+def test_fused_random_policy_matches_oracle(cuda, kernels, monkeypatch):
+    monkeypatch.setenv("BB_STEP_KERNELS", kernels)  # 1: fused (rollout kernel, T = 1); 2: step + escalate
     """bb_step's fused next_action == oracle Philox policy on the post-step mask."""
     from runtime.device_env import DeviceEnvBatch
 
@@ -148,7 +160,9 @@ def test_fused_random_policy_matches_oracle(cuda):
     dev.close()
 
 
-def test_hard_boards_escalate_to_wave_solver(cuda):
+@pytest.mark.parametrize("kernels", ["1", "2"])
+def test_hard_boards_escalate_to_wave_solver(cuda, kernels, monkeypatch):
+    monkeypatch.setenv("BB_STEP_KERNELS", kernels)  # 1: fused (rollout kernel, T = 1); 2: step + escalate
     """Crowded boards make many hand draws exceed the per-lane budget; the
     wave-cooperative path must give the same piece stream as the oracle."""
     from environment.wrappers import VectorizedBlockBlastEnv

@@ -108,9 +108,12 @@ def test_full_size_shard_unseeded_matches_c_oracle(cuda):
     assert _rollout_vs_oracle(cuda, N_FULL, 3 * N_FULL, launches=1, unseeded=unseeded) > 0
 
 
-def test_full_size_step_path_matches_c_oracle(cuda):
-    """bb_step (step_kernel + escalate_kernel) at 65,536 envs, 64 steps, the
-    VectorizedBlockBlastEnv.step drop-in path."""
+@pytest.mark.parametrize("kernels", ["1", "2"])
+def test_full_size_step_path_matches_c_oracle(cuda, kernels, monkeypatch):
+    """bb_step at 65,536 envs, 64 steps, the VectorizedBlockBlastEnv.step
+    drop-in path: fused (rollout kernel at T = 1, default) and step_kernel +
+    escalate_kernel (BB_STEP_KERNELS=2)."""
+    monkeypatch.setenv("BB_STEP_KERNELS", kernels)
     n, steps = N_FULL, 64
     env, seeds = _gpu_env(n, 0, cuda)
     cpu = _cpu_env(seeds)

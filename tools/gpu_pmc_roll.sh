@@ -21,7 +21,7 @@ for f in glob.glob(f"{out}/{tag}_*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r.get("Kernel_Name", "")
         for kn in ("step_kernel", "escalate_kernel", "rollout_kernel"):
-            if f"bb::{kn}(" in k:
+            if f"bb::{kn}(" in k or f"bb::{kn}<" in k:
                 acc[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (kn, c), v in sorted(acc.items()):
     print(f"{kn:16s} {c:22s} {sum(v)/len(v):16.1f}  (n={len(v)})")

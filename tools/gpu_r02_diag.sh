@@ -22,7 +22,7 @@ out, tag = sys.argv[1], sys.argv[2]
 acc = collections.defaultdict(list)
 for f in glob.glob(f"{out}/{tag}_sq*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "bb::rollout_kernel(" in r.get("Kernel_Name", ""):
+        if "bb::rollout_kernel" in r.get("Kernel_Name", ""):
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for c, v in sorted(acc.items()):
     print(f"{c:22s} {sum(v)/len(v):16.1f}  (n={len(v)})")

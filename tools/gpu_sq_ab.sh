@@ -21,7 +21,7 @@ for v in vs:
     acc = collections.defaultdict(list)
     for f in glob.glob(f"{out}/{tag}_{v}_*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "bb::rollout_kernel(" in r.get("Kernel_Name", ""):
+            if "bb::rollout_kernel" in r.get("Kernel_Name", ""):
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     ws = 2048 * 128  # wave-steps per launch (65,536 envs / 32 per wave, T = 128)
     print(v, " ".join(f"{c}={sum(x)/len(x)/ws:.1f}" for c, x in sorted(acc.items()) if c != "SQ_WAVES"), "(per wave-step)")

@@ -31,7 +31,7 @@ def per_kernel(d: str, counter: str, KERNELS):
                     continue
                 name = row.get("Kernel_Name", "")
                 for k in KERNELS:
-                    if f"bb::{k}(" in name:
+                    if f"bb::{k}(" in name or f"bb::{k}<" in name:
                         acc[k].append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items() if v}, {k: len(v) for k, v in acc.items()}
 
