@@ -182,6 +182,48 @@ __device__ __forceinline__ bool apply_move(const Tables& t, StepCtx& s, int act)
   return false;
 }
 
+// apply_move without branches (the rollout kernel): every quantity is computed
+// for the lane's action and committed by select, so the move is one basic
+// block the scheduler can interleave with the step's other independent work.
+// Same results as apply_move for every action, legal or not.
+__device__ __forceinline__ bool apply_move_bf(const Tables& t, StepCtx& s, int act) {
+  const bool inrange = (unsigned)act < 192u;
+  const int p = inrange ? (act >> 6) : 0;
+  const int cell = act & 63;
+  const uint32_t used0 = hand_used(s.hand);
+  const PieceRow& pr = t.row[hand_id(s.hand, p)];
+  const uint64_t placed = pr.shape << cell;
+  const bool valid = inrange && !hand_over(s.hand) && !((used0 >> p) & 1u) && ((pr.anchors >> cell) & 1ull) &&
+                     (placed & s.B) == 0ull;
+  const int nblk = (int)ncells_of(pr);
+  int rows, cols;
+  const uint64_t B2 = clear_full(s.B | placed, rows, cols);
+  const int lines = rows + cols;
+  const int combo1 = s.combo + 1;
+  const int cm = lines < 4 ? lines : 4;
+  const int streak = combo1 + 1 < 8 ? combo1 + 1 : 8;  // post-increment combo (engine.py:261)
+  const int64_t gained = lines > 0 ? nblk + (int64_t)(lines * 8 * 10) * cm * streak : (int64_t)nblk;
+  const bool clr = valid && lines > 0;
+  s.valid = valid;
+  s.nblk = valid ? nblk : 0;
+  s.lines = valid ? lines : 0;
+  s.cm = clr ? cm : 1;
+  s.gained = valid ? gained : 0;
+  s.B = valid ? B2 : s.B;
+  s.moves += valid ? 1 : 0;
+  s.blocks += valid ? nblk : 0;
+  s.max_combo = clr && combo1 > s.max_combo ? combo1 : s.max_combo;
+  s.combo = valid ? (lines > 0 ? combo1 : 0) : s.combo;
+  s.lines_tot += valid ? lines : 0;
+  s.score += valid ? gained : 0;
+  const uint32_t used = used0 | (1u << p);
+  const bool drew = valid && used == 7u;
+  s.drew = drew;
+  s.hand = !valid ? s.hand
+                  : (drew ? (s.hand & ~(7u << 18)) : ((s.hand & 0x3FFFFu) | (used << 18) | (s.hand & (1u << 22))));
+  return drew;
+}
+
 // ---------------------------------------------------------------------------
 // reset: engine.py:127-153 + block_blast_env.py:210-217
 // ---------------------------------------------------------------------------
@@ -612,6 +654,12 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 #ifndef BB_ROLL_SLOTS
 #define BB_ROLL_SLOTS 1  // in-lane quick-test slots per copy
 #endif
+#ifndef BB_ROLL_BFMOVE
+#define BB_ROLL_BFMOVE 1  // rollout: branch-free apply_move (apply_move_bf)
+#endif
+#ifndef BB_ROLL_PHILOX_TOP
+#define BB_ROLL_PHILOX_TOP 0  // rollout: the policy uniform drawn at the top of every step (no branch)
+#endif
 #ifndef BB_ROLL_KSTEP
 #define BB_ROLL_KSTEP BB_ROLL_SLOTS  // copy c tests slots c * KSTEP, c * KSTEP + 1, ...
 #endif
@@ -721,11 +769,24 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       partner = __hip_atomic_load(&prog[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // used next step
     }
 #endif
+#if BB_ROLL_PHILOX_TOP
+    // this step's policy uniform, independent of the env state: computed first, with no branch, so
+    // its Philox rounds interleave with the move; copy c draws step + 1 + c on even steps and the
+    // same counter again on odd steps
+    u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i,
+                             r.policy_step0 + (uint64_t)(step - step % kCopies) + 1 + half);
+    const uint32_t u_next = __shfl(u_drawn, (lane % kRollEnvs) + kRollEnvs * (step % kCopies));
+#endif
     BB_DIAG_T(c0);
     bool park = false;
     Pcg after = s.rng;  // stream state after attempt 1's draws
     if (live) {
-      if (apply_move(t, s, act)) {
+#if BB_ROLL_BFMOVE
+      const bool drew_now = apply_move_bf(t, s, act);
+#else
+      const bool drew_now = apply_move(t, s, act);
+#endif
+      if (drew_now) {
         uint32_t ids = 0;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 2  // timing diagnostics only: first draw, no test (NOT reference)
         ids = draw_piece(s.rng);
@@ -809,9 +870,11 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     }
 #endif
     BB_DIAG_T(c2);
+#if !BB_ROLL_PHILOX_TOP
     if (step % kCopies == 0)
       u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + step + 1 + half);
     const uint32_t u_next = __shfl(u_drawn, (lane % kRollEnvs) + kRollEnvs * (step % kCopies));
+#endif
     if (live) {
       masks_of(t, s.B, s.hand, m);
       double rew = -10.0;  // invalid action (block_blast_env.py:240-245)

@@ -26,6 +26,9 @@ VARIANTS = {
     # 64 envs per wave, one wave per SIMD (256-thread workgroups, no partner priority), in-lane slots 0|1
     "e64": ["-DBB_ROLL_ENVS=64", "-DBB_ROLL_BLOCK=256", "-DBB_ROLL_FAIR=0", "-DBB_ROLL_SLOTS=2"],
     "e64s1": ["-DBB_ROLL_ENVS=64", "-DBB_ROLL_BLOCK=256", "-DBB_ROLL_FAIR=0", "-DBB_ROLL_SLOTS=1"],
+    # rollout: branchy apply_move; policy Philox at the top of every step
+    "brmove": ["-DBB_ROLL_BFMOVE=0"],
+    "ptop": ["-DBB_ROLL_PHILOX_TOP=1"],
     # rollout SIMD-partner priority: 0 none, 1 alternate per step, 2 the wave behind takes it (shipped)
     "fair0": ["-DBB_ROLL_FAIR=0"],
     "fair1": ["-DBB_ROLL_FAIR=1"],
