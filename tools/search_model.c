@@ -146,6 +146,9 @@ typedef struct {
 } Stats;
 
 static int g_P = 1;
+static double* g_wave_cyc;  /* modelled search cycles per wave */
+static double g_call_max, g_heavy_cyc;
+static long g_heavy_n;
 static double g_cls[2][2], g_cls_n[2][2];  /* slow tasks by slot class: [one-sided][line reachable] */  /* passes (64 slots each) an attempt batch may span */
 
 static void model_call(Gen** par, int E0, int pack_first, int pack_next, Stats* st) {
@@ -328,6 +331,7 @@ int main(int argc, char** argv) {
   Stats st = {0};
   size_t parked = 0;
   Gen** grp = malloc(sizeof(Gen*) * 64);
+  g_wave_cyc = calloc(n / epw + 1, sizeof(double));
   size_t gi = 0;
   /* g_gens is in (t, i) order already (single-threaded replay) */
   while (gi < g_ngen) {
@@ -346,7 +350,19 @@ int main(int argc, char** argv) {
     }
     if (E) {
       parked += E;
+      const Stats before = st;
       model_call(grp, E, pack_first, pack_next, &st);
+      const double cyc = 3.63 * (st.rounds - before.rounds) + 3.83 * (st.passes - before.passes) +
+                         1.57 * (st.slow_rounds - before.slow_rounds);
+      g_wave_cyc[w] += cyc;
+      if (cyc > g_call_max) g_call_max = cyc;
+      if (cyc > 40.0) {
+        g_heavy_n++;
+        g_heavy_cyc += cyc;
+        if (g_heavy_n <= 8)
+          printf("heavy call: E=%d rounds %.0f passes %.0f slow %.0f -> %.0fk\n", E, st.rounds - before.rounds,
+                 st.passes - before.passes, st.slow_rounds - before.slow_rounds, cyc);
+      }
     }
   }
   const double wave_steps = (double)(n / epw) * T;
@@ -363,6 +379,16 @@ int main(int argc, char** argv) {
          (cr * st.rounds + cp * st.passes + cs * st.slow_rounds) / wave_steps);
   printf("slow tasks by slot class: both-sided %.0f (%.0f slots), one-sided reachable %.0f (%.0f), one-sided unreachable %.0f (%.0f)\n",
          g_cls[0][1], g_cls_n[0][1], g_cls[1][1], g_cls_n[1][1], g_cls[1][0], g_cls_n[1][0]);
+  {
+    const int nw = n / epw;
+    double mx = 0, mean = 0;
+    for (int w = 0; w < nw; ++w) { mean += g_wave_cyc[w]; if (g_wave_cyc[w] > mx) mx = g_wave_cyc[w]; }
+    mean /= nw;
+    const double base = 7.3 * T;  /* k-cycles of in-lane work per wave over T steps (GPU diag) */
+    printf("per wave over %d steps: search mean %.0fk max %.0fk; with in-lane base: max/mean %.3f; heaviest call %.1fk\n",
+           T, mean, mx, (mx + base) / (mean + base), g_call_max);
+  }
+  printf("calls above 40k cycles: %ld, %.1f%% of search cycles\n", g_heavy_n, 100.0 * g_heavy_cyc / (3.63 * st.rounds + 3.83 * st.passes + 1.57 * st.slow_rounds));
   printf("per env-step: modelled search %.1f cycles\n", (cr * st.rounds + cp * st.passes + cs * st.slow_rounds) * 1000 / wave_steps / epw);
   return 0;
 }
