@@ -657,6 +657,9 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 #ifndef BB_ROLL_BFMOVE
 #define BB_ROLL_BFMOVE 1  // rollout: branch-free apply_move (apply_move_bf)
 #endif
+#ifndef BB_ROLL_BFQUICK
+#define BB_ROLL_BFQUICK 1  // rollout: branch-free in-lane quick slot (quick_slot_bf)
+#endif
 #ifndef BB_ROLL_PHILOX_TOP
 #define BB_ROLL_PHILOX_TOP 0  // rollout: the policy uniform drawn at the top of every step (no branch)
 #endif
@@ -804,7 +807,11 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         uint32_t x0, x1, x2;
         draw3(s.rng, x0, x1, x2);
         ids = x0 | (x1 << 6) | (x2 << 12);
+#if BB_ROLL_BFQUICK && BB_ROLL_SLOTS == 1
+        park = !quick_slot_bf(s.B, x0, x1, x2, t.row, t.d, half * BB_ROLL_KSTEP);
+#else
         park = !quick_slots(s.B, x0, x1, x2, t.row, t.d, half * BB_ROLL_KSTEP, BB_ROLL_SLOTS);
+#endif
         after = s.rng;
         s.rng = save;  // the wave search redraws the attempt unless a half accepts
 #endif

@@ -231,6 +231,33 @@ __device__ __forceinline__ bool quick_slots(uint64_t B, uint32_t x0, uint32_t x1
   return false;
 }
 
+// quick_slots for one slot k without branches (the rollout kernel): the slot's
+// placement, both leaves and the |D| tests are all computed and combined, so
+// the whole test is one basic block (SIMT runs the leaves anyway whenever any
+// lane of the wave needs them).  Same verdict as quick_slots(B, .., k, 1).
+__device__ __forceinline__ bool quick_slot_bf(uint64_t B, uint32_t x0, uint32_t x1, uint32_t x2, const PieceRow* tbl,
+                                              const uint8_t* dtab, int k) {
+  const int f = k % 3;
+  const uint32_t fi = f == 0 ? x0 : (f == 1 ? x1 : x2);
+  const uint32_t bi = f == 0 ? x1 : x0;
+  const uint32_t ci = f == 2 ? x1 : x2;
+  const PieceRow& pf = tbl[fi];
+  const PieceRow& pb = tbl[bi];
+  const PieceRow& pc = tbl[ci];
+  const uint32_t dbc = dtab[bi * kPieces + ci];
+  const uint64_t Af = anchors_of(pf, B);
+  const int p = k < 3 ? __ffsll((unsigned long long)Af) - 1 : 63 - __clzll((long long)(Af | 1ull));
+  const uint64_t B1 = clear_full(B | (pf.shape << (p & 63)));
+  const uint64_t A2 = anchors_of(pb, B1);
+  const uint64_t A3 = anchors_of(pc, B1);
+  const bool dacc = (A2 && (uint32_t)__popcll(A3) > dbc) || (A3 && (uint32_t)__popcll(A2) > dbc);
+  const int q = __ffsll((unsigned long long)A2) - 1;
+  const int r = __ffsll((unsigned long long)A3) - 1;
+  const bool leaf2 = A2 && anchors_of(pc, clear_full(B1 | (pb.shape << (q & 63)))) != 0ull;
+  const bool leaf3 = A3 && anchors_of(pb, clear_full(B1 | (pc.shape << (r & 63)))) != 0ull;
+  return Af != 0ull && (dacc || leaf2 || leaf3);
+}
+
 // In-lane quick test of the first attempt (step_kernel): draw its three
 // pieces and test up to `slots` fixed level-1 slots -- first piece f = k mod 3
 // at its lowest (k < 3) or highest anchor -- with pair_quick.  Straight-line
