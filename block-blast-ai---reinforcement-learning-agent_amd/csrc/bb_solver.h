@@ -208,6 +208,19 @@ __device__ __forceinline__ int pair_quick_nc(uint64_t B1, const PieceRow& pb, co
   return 2;
 }
 
+// pair_quick without branches: 0 reject, 1 accept, 2 undecided, A2 / A3 out.
+__device__ __forceinline__ int pair_quick_bf(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint32_t dbc,
+                                             uint64_t& A2, uint64_t& A3) {
+  A2 = anchors_of(pb, B1);
+  A3 = anchors_of(pc, B1);
+  const bool dacc = (A2 && (uint32_t)__popcll(A3) > dbc) || (A3 && (uint32_t)__popcll(A2) > dbc);
+  const int q = __ffsll((unsigned long long)A2) - 1;
+  const int r = __ffsll((unsigned long long)A3) - 1;
+  const bool leaf2 = A2 && anchors_of(pc, clear_full(B1 | (pb.shape << (q & 63)))) != 0ull;
+  const bool leaf3 = A3 && anchors_of(pb, clear_full(B1 | (pc.shape << (r & 63)))) != 0ull;
+  return (A2 | A3) == 0ull ? 0 : ((dacc || leaf2 || leaf3) ? 1 : 2);
+}
+
 // Quick test of fixed level-1 slots k0 .. k0+slots-1 of the drawn hand
 // (x0, x1, x2) on B: slot k places piece k mod 3 at its lowest (k < 3) or
 // highest anchor, then pair_quick.  True on an accept (an exact success).
@@ -548,6 +561,9 @@ constexpr int kPack = 32;
 #define BB_MULTI_PASSES 3  // gen_hands_multi: a round packs attempts for up to this many 64-slot passes
 #endif
 constexpr int kMultiPasses = BB_MULTI_PASSES;
+#ifndef BB_PASS_BF
+#define BB_PASS_BF 1  // gen_hands_multi passes: slot decode + pair test without branches (pair_quick_bf)
+#endif
 #ifndef BB_PASS_NC
 #define BB_PASS_NC 0  // 1: pass leaf tests without the line clear (pair_quick_nc; measured slower: more exact-phase work)
 #endif
@@ -884,6 +900,21 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       int q = 0;
       uint64_t B1 = 0, A2 = 0, A3 = 0;
       uint32_t bi = 0, ci = 0;
+#if BB_PASS_BF
+      {  // every lane computes its slot (lanes past `total` a dummy one) and drops it by select
+        const int rem0 = slot - joff;
+        const int c0 = __popcll(jA0), c1 = __popcll(jA1);
+        const int f = rem0 < c0 ? 0 : (rem0 < c0 + c1 ? 1 : 2);
+        const uint64_t Af = f == 0 ? jA0 : (f == 1 ? jA1 : jA2);
+        const int rem = rem0 - (f == 0 ? 0 : (f == 1 ? c0 : c0 + c1));
+        const int p = select_bit(Af, (uint32_t)rem) & 63;
+        bi = hand_id(jid, f == 0 ? 1 : 0);
+        ci = hand_id(jid, f == 2 ? 1 : 2);
+        B1 = clear_full(jB | (tbl[hand_id(jid, f)].shape << p));
+        q = pair_quick_bf(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
+        if (slot >= total) q = 0;
+      }
+#else
       if (slot < total) {
         int rem = slot - joff;
         const int c0 = __popcll(jA0), c1 = __popcll(jA1);
@@ -911,6 +942,7 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
         q = pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
 #endif
       }
+#endif
       // attempt lanes with a quick accept: attempt lane L owns the pass's slot
       // bits [lo, hi) of any slot ballot
       const int lo = e_off > base ? e_off - base : 0;

@@ -30,6 +30,7 @@ VARIANTS = {
     "brmove": ["-DBB_ROLL_BFMOVE=0"],
     "ptop": ["-DBB_ROLL_PHILOX_TOP=1"],
     "brquick": ["-DBB_ROLL_BFQUICK=0"],
+    "brpass": ["-DBB_PASS_BF=0"],
     # rollout SIMD-partner priority: 0 none, 1 alternate per step, 2 the wave behind takes it (shipped)
     "fair0": ["-DBB_ROLL_FAIR=0"],
     "fair1": ["-DBB_ROLL_FAIR=1"],
