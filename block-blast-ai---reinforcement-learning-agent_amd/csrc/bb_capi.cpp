@@ -634,3 +634,54 @@ extern "C" int bb_ppo_loss_backward(const float* d_logits, const float* d_values
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_ppo_loss_backward");
   return BB_OK;
 }
+
+namespace {
+int conv_check(int32_t N, int32_t cin, int32_t cout, const char* what) {
+  if (N <= 0) return fail(nullptr, BB_ERR_ARG, std::string(what) + ": empty batch");
+  if (!conv3x3_supported(cin, cout))
+    return fail(nullptr, BB_ERR_ARG, std::string(what) + ": channels must be 64 or 128 in and out");
+  return BB_OK;
+}
+bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+}  // namespace
+
+extern "C" int64_t bb_conv3x3_workspace_bytes(int32_t N, int32_t cin, int32_t cout) {
+  if (conv_check(N, cin, cout, "bb_conv3x3_workspace_bytes") != BB_OK) return -1;
+  return conv3x3_wgrad_workspace_bytes(N, cin, cout);
+}
+
+extern "C" int bb_conv3x3_prep(const float* d_w, int32_t cin, int32_t cout, int32_t w_layout, void* d_wf, void* d_wd,
+                               void* stream) {
+  int rc = conv_check(1, cin, cout, "bb_conv3x3_prep");
+  if (rc != BB_OK) return rc;
+  if (w_layout != 0 && w_layout != 1) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_prep: w_layout must be 0 or 1");
+  if (!d_w || !d_wf || !d_wd) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_prep: NULL argument");
+  if (!al16(d_wf) || !al16(d_wd)) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_prep: outputs must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_prep(d_w, cin, cout, w_layout, d_wf, d_wd, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_prep");
+  return BB_OK;
+}
+
+extern "C" int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
+                                  void* stream) {
+  int rc = conv_check(N, cin, cout, "bb_conv3x3_forward");
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_w || !d_y) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward: NULL argument");
+  if (!al16(d_x) || !al16(d_w) || !al16(d_y))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward: tensors must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward");
+  return BB_OK;
+}
+
+extern "C" int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
+                                int32_t w_layout, float* d_dw, void* stream) {
+  int rc = conv_check(N, cin, cout, "bb_conv3x3_wgrad");
+  if (rc != BB_OK) return rc;
+  if (w_layout != 0 && w_layout != 1) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_wgrad: w_layout must be 0 or 1");
+  if (!d_x || !d_dy || !d_ws || !d_dw) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_wgrad: NULL argument");
+  if (!al16(d_x) || !al16(d_dy)) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_wgrad: tensors must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_wgrad(d_x, d_dy, N, cin, cout, d_ws, w_layout, d_dw, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_wgrad");
+  return BB_OK;
+}

@@ -1,0 +1,528 @@
+// bb_conv.hip -- the CNN's 3x3 / pad-1 convolutions on 8x8 board planes, bf16
+// MFMA with f32 accumulation (gfx950).
+//
+// BlockBlastNetwork's conv stack (network.py:75-117, ResidualBlock
+// network.py:14-30) is conv 4->64, conv 64->128 and five conv 128->128, all
+// 3x3 with padding 1 over 8x8 boards.  Under bf16 autocast MIOpen ran the
+// 128-channel layers at 0.4-0.7 PFLOP/s and its split-K weight gradient needed
+// zero fills and casts around it (the PPO optimizer step).  These
+// kernels are written for the 8x8 board: a board is 64 pixel rows of C channels
+// in NHWC, the nine taps are row shifts inside a board, and a tap that leaves
+// the board reads a zero row of LDS instead of branching.
+//
+//   forward  y[b,p,co]  = sum_{t,ci} x[b,p+d_t,ci] * w[co,ci,t]
+//   data grad dx[b,q,ci] = sum_{t,co} dy[b,q-d_t,co] * w[co,ci,t]
+//            = the forward kernel over dy with w'[t'][ci][co] = w[co][ci][8-t']
+//   weight grad dw[co,ci,t] = sum_{b,p} dy[b,p,co] * x[b,p+d_t,ci]
+// with d_t = (t/3 - 1, t%3 - 1) and zero outside the board.  Activations are
+// bf16 NHWC (channels_last), weights f32 [Cout][Cin][3][3] (nn.Conv2d) cast to
+// bf16 with round-to-nearest-even as autocast does, accumulation f32, y and dx
+// rounded to bf16, dw f32.  The weight gradient is split over board chunks
+// into f32 partials that one pass adds in a fixed order: no atomics, results
+// are deterministic run to run.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "bb_env_internal.h"
+
+namespace bb {
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+constexpr int kThreads = 256;
+constexpr int kFwdBoards = 2;    // forward: 128 pixel rows per workgroup
+constexpr int kWgBoards = 2;     // weight grad: boards per LDS stage
+constexpr int kWgTile = 64;      // weight grad: 64 x 64 (co, ci) tile, all nine taps
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);  // round to nearest even
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+}
+
+// ---------------------------------------------------------------------------
+// weight prep: w f32 [COUT][CIN][9] (wl 0) or [COUT][9][CIN] (wl 1, a
+// channels_last parameter) -> wf bf16 [9][COUT][CIN] (forward) and wd bf16
+// [9][CIN][COUT] with tap 8 - t (data gradient)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) conv_prep_kernel(const float* __restrict__ w, int cout, int cin, int wl,
+                                                             uint16_t* __restrict__ wf, uint16_t* __restrict__ wd) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= cout * cin * 9) return;
+  const int co = i / (9 * cin);
+  const int t = wl ? (i / cin) % 9 : i % 9;
+  const int ci = wl ? i % cin : (i / 9) % cin;
+  const uint16_t b = f2bf(w[i]);
+  wf[(t * cout + co) * cin + ci] = b;
+  wd[((8 - t) * cin + ci) * cout + co] = b;
+}
+
+// LDS image of pixel rows of C bf16 channels: 16-byte chunk c of row r sits at
+// chunk c ^ key(r), so 16 lanes reading one chunk of 16 consecutive rows hit
+// 16 different bank groups (256-B rows: key = r & 15; 128-B rows, two per bank
+// line: key = (r >> 1) & 7).
+template <int C>
+__device__ __forceinline__ int fwd_key(int r) {
+  return C == 128 ? (r & 15) : ((r >> 1) & 7);
+}
+
+// Direct global -> LDS copy of one 16-byte chunk per lane: lane L of the wave
+// lands at lds_base + 16 L (lds_base wave-uniform); the global address is per
+// lane, so swizzled LDS images are written by permuting the sources.
+__device__ __forceinline__ void glds16(const void* g, uint8_t* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// The same copy issued from inline asm: the compiler then does not track it,
+// so it inserts no vmcnt(0) before LDS reads of OTHER buffers while it is in
+// flight; the caller waits for it with a counted BB_WAIT_VM before the barrier
+// that precedes reading its buffer.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else in these kernels keeps it live
+__device__ __forceinline__ void glds16_async(const void* g, uint8_t* lds_base) {
+  const uint32_t l = (uint32_t)(size_t)((__attribute__((address_space(3))) uint8_t*)lds_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// s_waitcnt with vmcnt = n (expcnt, lgkmcnt not waited)
+#define BB_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (7 << 4) | (15 << 8) | (((n) >> 4) << 14))
+// s_waitcnt with vmcnt = n and lgkmcnt = 0
+#define BB_WAIT_VM_LGKM0(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (7 << 4) | (((n) >> 4) << 14))
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// forward / data gradient.  Workgroup (4 waves): 2 boards = 128 pixel rows x
+// all COUT; two workgroups share a CU, so one's copies and barriers overlap
+// the other's MFMAs.  D[co][px] = sum_k W[co][k] X[k][px] on
+// mfma_f32_32x32x16_bf16 with A = the weights, B = the (shifted) input rows,
+// both from LDS (ds_read_b128), the fragments of k-step k+1 read while k
+// computes; each lane ends with 4 consecutive output channels of one pixel per
+// register group (8-byte stores).  The input tile is copied once (direct
+// global -> LDS).  The weights stream from L2 in stages of one tap x 32 input
+// channels (COUT rows of 64 B) through a ring of kFwdRing LDS buffers, copied
+// kFwdRing - 1 stages ahead; each wave waits (counted vmcnt) only for its own
+// copies of the next stage before the barrier.
+// Waves: COUT = 128 -> 2 (co) x 2 (px) waves of 64 co x 64 px;
+//        COUT =  64 -> 1 x 4 waves of 64 co x 32 px.
+// A tap that leaves the board reads one of 16 zero rows, the one whose
+// swizzle matches the row it replaces (no extra bank conflict).  Boards past
+// the batch read board nb-1 (their outputs are not stored; taps never cross
+// boards).  Weight rows of 64 B hold 16-byte chunk c at c ^ ((co >> 2) & 3).
+// ---------------------------------------------------------------------------
+constexpr int kFwdThreads = 256;
+constexpr int kZeroRows = 16;
+#ifndef BB_CONV_FWD_RING
+#define BB_CONV_FWD_RING 2  // 3: -29%, 5 with 32-channel stages: -14% (tools/variants.py cf*)
+#endif
+#ifndef BB_CONV_FWD_SCI
+#define BB_CONV_FWD_SCI 64
+#endif
+#ifndef BB_CONV_DIAG
+#define BB_CONV_DIAG 0  // diagnostics only: 1 = no output stores, 2 = one tap of the nine
+#endif
+constexpr int kFwdRing = BB_CONV_FWD_RING;
+
+template <int SCI>
+__device__ __forceinline__ int wkey(int co) {
+  return SCI == 32 ? (co >> 2) & 3 : (co >> 1) & 7;
+}
+
+template <int CIN, int COUT>
+__global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* __restrict__ x,
+                                                               const uint16_t* __restrict__ w,
+                                                               uint16_t* __restrict__ y, int nb) {
+  constexpr int RB = CIN * 2;                 // bytes per pixel row
+  constexpr int NCH = CIN / 8;                // 16-byte chunks per pixel row
+  constexpr int ROWS = kFwdBoards * 64;       // 128
+  constexpr int XBYTES = (ROWS + kZeroRows) * RB;
+  constexpr int SCI = BB_CONV_FWD_SCI;        // input channels per weight stage (32 or 64)
+  constexpr int NCB = CIN / SCI;              // stages per tap
+  constexpr int NS = (BB_CONV_DIAG == 2 ? 1 : 9) * NCB;  // stages
+  constexpr int WBYTES = COUT * SCI * 2;      // one stage: COUT rows of SCI * 2 bytes
+  constexpr int NW = kFwdThreads / 64;        // 4 waves
+  constexpr int GPW = WBYTES / 1024 / NW;     // weight copies per wave per stage
+  constexpr int DIST = kFwdRing - 1;          // stages in flight ahead
+  constexpr int WN = COUT / 64;               // waves along co
+  constexpr int WM = NW / WN;                 // waves along px
+  constexpr int TM = (ROWS / WM) / 32;        // 32-px MFMA tiles per wave
+  constexpr int TN = 2;                       // 32-co MFMA tiles per wave
+  constexpr int KK = SCI / 16;                // k-steps per stage
+  static_assert(GPW >= 1, "weight stage smaller than one copy per wave");
+  __shared__ __attribute__((aligned(16))) uint8_t sm[XBYTES + kFwdRing * WBYTES];
+  uint8_t* const xs = sm;
+
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int b0 = blockIdx.x * kFwdBoards;
+
+  // input tile: LDS chunk e = 64 k + lane holds row e / NCH, logical chunk (e % NCH) ^ key(row)
+#pragma unroll
+  for (int k = wid; k < ROWS * NCH / 64; k += NW) {
+    const int e = k * 64 + lane, r = e / NCH, lc = (e % NCH) ^ fwd_key<CIN>(r);
+    const int b = min(b0 + (r >> 6), nb - 1);
+    glds16_async(x + (size_t(b) * 64 + (r & 63)) * CIN + lc * 8, xs + k * 1024);
+  }
+  // weight stage st (tap st / NCB, channels 32 (st % NCB) ...) -> ring slot st % kFwdRing
+  auto stage_w = [&](int st) {
+    uint8_t* wb = sm + XBYTES + (st % kFwdRing) * WBYTES;
+    const uint16_t* ws = w + (size_t)(st / NCB) * COUT * CIN + (st % NCB) * SCI;
+#pragma unroll
+    for (int kq = 0; kq < GPW; ++kq) {
+      const int k = wid + kq * NW;
+      const int e = k * 64 + lane, r = e / (SCI / 8), lc = (e % (SCI / 8)) ^ wkey<SCI>(r);
+      glds16_async(ws + r * CIN + lc * 8, wb + k * 1024);
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < DIST; ++st) stage_w(st);
+  for (int i = tid; i < kZeroRows * NCH; i += kFwdThreads)
+    *reinterpret_cast<uint4*>(xs + ROWS * RB + i * 16) = make_uint4(0, 0, 0, 0);
+  BB_WAIT_VM_LGKM0((DIST - 1) * GPW);  // the input tile and stage 0 have landed
+  raw_barrier();
+
+  const int r = lane & 31, h = lane >> 5;
+  const int co0 = (wid % WN) * 64;
+  const int px0 = (wid / WN) * (ROWS / WM);
+  int abase[TN], akey[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int co = co0 + 32 * j + r;
+    abase[j] = co * SCI * 2;
+    akey[j] = wkey<SCI>(co);
+  }
+
+  f32x16 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+
+  int rb[TM], key[TM];
+  for (int st = 0; st < NS; ++st) {
+    if (st + DIST < NS) stage_w(st + DIST);  // its slot was last read in stage st-1, before the barrier
+    const int cb = st % NCB;
+    if (cb == 0) {
+      const int t = st / NCB, dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int px = px0 + 32 * i + r;
+        const int p = px & 63, yy = (p >> 3) + dy, xc = (p & 7) + dx;
+        const int row = ((unsigned)yy < 8u && (unsigned)xc < 8u) ? (px & ~63) + yy * 8 + xc
+                                                                  : ROWS + ((px + 8 * dy + dx) & 15);
+        rb[i] = row * RB;
+        key[i] = fwd_key<CIN>(row);
+      }
+    }
+    const uint8_t* wb = sm + XBYTES + (st % kFwdRing) * WBYTES;
+    bf16x8 afr[2][TN], bfr[2][TM];
+    auto load = [&](int kk, int set) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        afr[set][j] = *reinterpret_cast<const bf16x8*>(wb + abase[j] + (((2 * kk + h) ^ akey[j]) << 4));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        bfr[set][i] = *reinterpret_cast<const bf16x8*>(xs + rb[i] + (((cb * (SCI / 8) + 2 * kk + h) ^ key[i]) << 4));
+    };
+    load(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      // the reads of k-step kk+1 are issued before the MFMAs of kk (the scheduler
+      // would otherwise reuse the registers and wait on every k-step's reads)
+      if (kk + 1 < KK) load(kk + 1, (kk + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[kk & 1][j], bfr[kk & 1][i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the next stage must have landed: this wave's copies (counted), the others' (barrier)
+    const int after = min(NS, st + DIST + 1) - (st + 2);
+    if (after >= 4) BB_WAIT_VM(4 * GPW);
+    else if (after == 3) BB_WAIT_VM(3 * GPW);
+    else if (after == 2) BB_WAIT_VM(2 * GPW);
+    else if (after == 1) BB_WAIT_VM(GPW);
+    else BB_WAIT_VM(0);
+    raw_barrier();
+  }
+
+  // epilogue: lane holds D[co0 + 32j + 8g + 4h + (0..3)][px0 + 32i + r]
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int px = px0 + 32 * i + r;
+    if (b0 + (px >> 6) >= nb) continue;
+    if (BB_CONV_DIAG == 1 && acc[0][i][0] != 1.2345e-30f) continue;
+    uint16_t* yo = y + (size_t(b0) * 64 + px) * COUT + co0 + 4 * h;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 v;
+        v.x = pack2(acc[j][i][4 * g + 0], acc[j][i][4 * g + 1]);
+        v.y = pack2(acc[j][i][4 * g + 2], acc[j][i][4 * g + 3]);
+        *reinterpret_cast<uint2*>(yo + 32 * j + 8 * g) = v;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient.  Workgroup (8 waves): one 64 (co) x 64 (ci) tile, all nine
+// taps, over a chunk of boards, 2 boards per LDS stage.  Stages go through a
+// ring of 4 LDS buffers by direct global -> LDS copies issued 3 stages ahead;
+// each wave waits (counted vmcnt) only for its copies of the next stage before
+// the barrier, so the HBM latency of a stage is covered by three stages of
+// MFMAs.  Both operands have the pixel as their k index, so they are read with
+// ds_read_b64_tr_b16 from plain NHWC rows (the hardware transposes 4 rows x 16
+// channels per 16-lane group); the shifted input rows of a tap point at a zero
+// row when they leave the board.  Waves 4k + (wc, wi) take board k of each
+// stage and accumulate D_t[32 co][32 ci] for the nine taps (144 f32 per lane);
+// at the end the second half hands its sums to the first through LDS, which
+// writes the chunk's partial [chunk][t][co][ci]; conv_wgrad_reduce adds the
+// chunks in order.  The grid runs the 4 tiles of a chunk next to each other,
+// so the second read of each slice of dy and x comes from cache.
+// LDS rows are 128 B (64 channels); 8-byte unit u of row r sits at
+// u ^ (((r >> 1) & 1) << 3), which makes a 32-lane half's 4 consecutive rows x
+// 32 channels conflict-free; the 4 zero rows follow the same pattern, and an
+// off-board row v reads zero row v & 3 (the bank segment v would have used).
+// ---------------------------------------------------------------------------
+constexpr int kWgThreads = 512;
+constexpr int kWgRing = 4;
+
+__device__ __forceinline__ int wg_off(int r, int u) { return r * 128 + ((u ^ (((r >> 1) & 1) << 3)) << 3); }
+
+template <int CIN, int COUT>
+__global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* __restrict__ x,
+                                                                const uint16_t* __restrict__ dy,
+                                                                float* __restrict__ part, int nb, int bpc) {
+  constexpr int SROWS = kWgBoards * 64;                // pixel rows per stage and operand
+  constexpr int SBYTES = 2 * SROWS * 128;              // dy rows then x rows
+  constexpr int ZOFF = kWgRing * SBYTES;               // 4 zero rows after the ring
+  constexpr int NWAVE = kWgThreads / 64;
+  constexpr int GPS = SBYTES / 1024 / NWAVE;           // copies per wave per stage (4)
+  __shared__ __attribute__((aligned(16))) uint8_t sm[kWgRing * SBYTES + 4 * 128];
+
+  constexpr int TCI = CIN / kWgTile;
+  const int tile = blockIdx.x;
+  const int co_t = (tile / TCI) * kWgTile, ci_t = (tile % TCI) * kWgTile;
+  const int chunk = blockIdx.y;
+  const int bb = chunk * bpc;
+  const int be = min(nb, bb + bpc);
+  const int nst = (be - bb + kWgBoards - 1) / kWgBoards;
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if (tid < 32) *reinterpret_cast<uint4*>(sm + ZOFF + tid * 16) = make_uint4(0, 0, 0, 0);
+
+  // stage copy: wave-instruction k (1 KB = 8 rows of 128 B) of [operand][row];
+  // lane L -> row 8k' + L/8, physical 16-byte chunk L%8 = logical chunk ^ 4*((row>>1)&1)
+  auto stage = [&](int si) {
+    const int s0 = bb + si * kWgBoards;
+    uint8_t* base = sm + (si & (kWgRing - 1)) * SBYTES;
+#pragma unroll
+    for (int kq = 0; kq < GPS; ++kq) {
+      const int k = wid + kq * NWAVE;
+      const int op = k / (SROWS / 8), r = (k % (SROWS / 8)) * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ ((((r >> 1) & 1)) << 2);
+      const int b = min(s0 + (r >> 6), nb - 1);  // past the chunk: any valid board, skipped below
+      const size_t pix = size_t(b) * 64 + (r & 63);
+      const uint16_t* src = op == 0 ? dy + pix * COUT + co_t + lc * 8 : x + pix * CIN + ci_t + lc * 8;
+      glds16_async(src, base + k * 1024);
+    }
+  };
+
+  const int half = wid >> 2, wc = wid & 1, wi = (wid >> 1) & 1;
+  const int gi = lane & 15, g = lane >> 4, hh = g >> 1, q = gi >> 2, p = gi & 3;
+  const int ucol = (g & 1) * 4 + p;   // 8-byte unit within the wave's 32 channels
+  const int ua = wc * 8 + ucol;       // dy unit (co)
+  const int ub = wi * 8 + ucol;       // x unit (ci)
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+
+  const int pre = min(nst, kWgRing - 1);
+  for (int si = 0; si < pre; ++si) stage(si);
+  // stage 0 landed (the later ones may still be in flight), zero rows written
+  if (pre == 3) BB_WAIT_VM_LGKM0(2 * GPS);
+  else if (pre == 2) BB_WAIT_VM_LGKM0(GPS);
+  else BB_WAIT_VM_LGKM0(0);
+  raw_barrier();
+  for (int si = 0; si < nst; ++si) {
+    if (si + kWgRing - 1 < nst) stage(si + kWgRing - 1);  // its buffer was last read in stage si-1
+    const int s0 = bb + si * kWgBoards;
+    if (s0 + half < be) {
+      const int sdy = (si & (kWgRing - 1)) * SBYTES + half * 64 * 128;
+      const int sx = sdy + SROWS * 128;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        // this lane's rows of the two transposed reads: board-local pixels 16ks + 8hh + q (+4), board row 2ks + hh
+        const int o0 = 16 * ks + 8 * hh + q;
+        const bf16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + sdy + wg_off(o0, ua)));
+        const bf16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + sdy + wg_off(o0 + 4, ua)));
+        const bf16x8 afr = __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7);
+        const int yy0 = 2 * ks + hh;
+        auto bload = [&](int t) {
+          const int ddy = t / 3 - 1, ddx = t % 3 - 1;
+          const int iy = yy0 + ddy, ix0 = q + ddx, ix1 = q + 4 + ddx;
+          const bool vy = (unsigned)iy < 8u;
+          const int v0 = iy * 8 + ix0, v1 = iy * 8 + ix1;
+          const int off0 = (vy && (unsigned)ix0 < 8u) ? sx + wg_off(v0, ub) : ZOFF + wg_off(v0 & 3, ub);
+          const int off1 = (vy && (unsigned)ix1 < 8u) ? sx + wg_off(v1, ub) : ZOFF + wg_off(v1 & 3, ub);
+          const bf16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off0));
+          const bf16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off1));
+          return __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
+        };
+        bf16x8 bfr[2];
+        bfr[0] = bload(0);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          if (t + 1 < 9) bfr[(t + 1) & 1] = bload(t + 1);  // in flight while tap t's MFMA issues
+          __builtin_amdgcn_sched_barrier(0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[t & 1], acc[t], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    // the next stage must have landed (this wave's copies; the barrier covers the others')
+    const int after = min(nst, si + kWgRing) - (si + 2);  // stages issued after stage si+1
+    if (after >= 2) BB_WAIT_VM(2 * GPS);
+    else if (after == 1) BB_WAIT_VM(GPS);
+    else BB_WAIT_VM(0);
+    raw_barrier();
+  }
+
+  // the second half's sums -> LDS (3 taps = 48 KB at a time) -> added by the first half
+  const int r = lane & 31, h = lane >> 5;
+  float* pp = part + (size_t)chunk * 9 * COUT * CIN;
+  float* red = reinterpret_cast<float*>(sm);
+  const int slot = (wid & 3) * 64 + lane;  // the partner waves (wid, wid + 4) share a slot
+#pragma unroll
+  for (int t0 = 0; t0 < 9; t0 += 3) {
+    if (half == 1) {
+#pragma unroll
+      for (int t = t0; t < t0 + 3; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[((t - t0) * 16 + e) * 256 + slot] = acc[t][e];
+    }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+      for (int t = t0; t < t0 + 3; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int co = co_t + 32 * wc + (e & 3) + 8 * (e >> 2) + 4 * h;
+          pp[((size_t)t * COUT + co) * CIN + ci_t + 32 * wi + r] = acc[t][e] + red[((t - t0) * 16 + e) * 256 + slot];
+        }
+    }
+    __syncthreads();
+  }
+}
+
+// dw[co][ci][t] (wl 0) or dw[co][t][ci] (wl 1) = sum over chunks, in chunk order
+__global__ void __launch_bounds__(kThreads) conv_wgrad_reduce(const float* __restrict__ part, int nchunk, int cout,
+                                                              int cin, int wl, float* __restrict__ dw) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;  // over [t][co][ci]
+  const int n = 9 * cout * cin;
+  if (i >= n) return;
+  float s = 0.f;
+  int c = 0;
+  for (; c + 16 <= nchunk; c += 16) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = part[(size_t)(c + k) * n + i];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += v[k];
+  }
+  for (; c < nchunk; ++c) s += part[(size_t)c * n + i];
+  const int ci = i % cin, co = (i / cin) % cout, t = i / (cin * cout);
+  dw[wl ? (co * 9 + t) * cin + ci : (co * cin + ci) * 9 + t] = s;
+}
+
+int wgrad_chunks(int nb, int cin, int cout) {
+  const int tiles = (cin / kWgTile) * (cout / kWgTile);
+  int nchunk = 256 / tiles;  // one 8-wave workgroup per CU
+  const int maxc = (nb + kWgBoards - 1) / kWgBoards;
+  if (nchunk > maxc) nchunk = maxc;
+  if (nchunk < 1) nchunk = 1;
+  return nchunk;
+}
+
+int wgrad_bpc(int nb, int nchunk) {
+  int bpc = (nb + nchunk - 1) / nchunk;
+  return (bpc + kWgBoards - 1) / kWgBoards * kWgBoards;
+}
+
+template <int CIN, int COUT>
+hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s) {
+  hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + kFwdBoards - 1) / kFwdBoards), dim3(kFwdThreads), 0, s,
+                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb);
+  return hipGetLastError();
+}
+
+template <int CIN, int COUT>
+hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s) {
+  const int nchunk = wgrad_chunks(nb, CIN, COUT);
+  const int bpc = wgrad_bpc(nb, nchunk);
+  const int used = (nb + bpc - 1) / bpc;  // chunks that hold boards
+  hipLaunchKernelGGL((conv_wgrad_kernel<CIN, COUT>), dim3((CIN / kWgTile) * (COUT / kWgTile), used), dim3(kWgThreads),
+                     0, s, (const uint16_t*)x, (const uint16_t*)dy, ws, nb, bpc);
+  hipError_t st = hipGetLastError();
+  if (st != hipSuccess) return st;
+  const int n = 9 * COUT * CIN;
+  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ws, used, COUT,
+                     CIN, wl, dw);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool conv3x3_supported(int cin, int cout) {
+  return (cin == 64 || cin == 128) && (cout == 64 || cout == 128);
+}
+
+int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout) {
+  const int nchunk = wgrad_chunks(nb, cin, cout);
+  return (int64_t)nchunk * 9 * cin * cout * (int64_t)sizeof(float);
+}
+
+hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* wf, void* wd, hipStream_t s) {
+  const int n = cout * cin * 9;
+  hipLaunchKernelGGL(conv_prep_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, w, cout, cin, wl,
+                     (uint16_t*)wf, (uint16_t*)wd);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s) {
+  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s);
+  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s);
+  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s);
+  return fwd_t<128, 128>(x, w, nb, y, s);
+}
+
+hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
+                                float* dw, hipStream_t s) {
+  if (cin == 64 && cout == 64) return wgrad_t<64, 64>(x, dy, nb, ws, wl, dw, s);
+  if (cin == 64 && cout == 128) return wgrad_t<64, 128>(x, dy, nb, ws, wl, dw, s);
+  if (cin == 128 && cout == 64) return wgrad_t<128, 64>(x, dy, nb, ws, wl, dw, s);
+  return wgrad_t<128, 128>(x, dy, nb, ws, wl, dw, s);
+}
+
+}  // namespace bb

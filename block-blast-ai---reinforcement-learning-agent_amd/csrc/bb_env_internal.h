@@ -101,6 +101,13 @@ hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
                               int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s);
 
+bool conv3x3_supported(int cin, int cout);
+int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout);
+hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* wf, void* wd, hipStream_t s);
+hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s);
+hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
+                                float* dw, hipStream_t s);
+
 int64_t ppo_loss_workspace_bytes(int B);
 hipError_t launch_ppo_loss_forward(const float* logits, const float* values, const float* mask, const int64_t* actions,
                                    const float* old_logp, const float* adv, const float* ret, int B, float clip,

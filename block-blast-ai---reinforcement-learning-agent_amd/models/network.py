@@ -10,6 +10,7 @@ csrc/bb_ppo.hip) used on the rollout path.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -55,13 +56,30 @@ class BatchNorm2d(nn.BatchNorm2d):
         return F.relu(y) if self.fuse_relu else y
 
 
+HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs on csrc/bb_conv.hip under bf16
+
+
+def conv_nobias(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """conv(x) without its bias.  Under bf16 autocast on the GPU the 3x3
+    layers with 64 or 128 channels in and out run on the HIP kernels
+    (runtime.kernels.Conv3x3Function): bf16 NHWC, f32 accumulation, as
+    autocast's conv2d."""
+    if HIP_CONV and x.is_cuda and torch.is_autocast_enabled("cuda") \
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+        from runtime.kernels import Conv3x3Function, conv3x3_fusable
+
+        if conv3x3_fusable(x, conv):
+            return Conv3x3Function.apply(x, conv.weight)
+    return conv._conv_forward(x, conv.weight, None)
+
+
 def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """bn(conv(x)).  When the BatchNorm runs on the HIP kernels the
     convolution's bias is added inside them (one add on load instead of a
     separate pass, and its gradient comes out of the BatchNorm backward instead
     of a reduction over dy)."""
     if isinstance(bn, BatchNorm2d) and conv.bias is not None and bn.training and x.is_cuda and bn.use_fused:
-        z = conv._conv_forward(x, conv.weight, None)
+        z = conv_nobias(conv, x)
         if bn.fusable(z):
             return bn(z, pre_bias=conv.bias)
         return bn(z + conv.bias.view(1, -1, 1, 1).to(z.dtype))

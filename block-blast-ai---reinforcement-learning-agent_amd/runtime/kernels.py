@@ -200,6 +200,75 @@ class BatchNormReLUFunction(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------------------
+# 3x3 / pad-1 convolutions over 8x8 boards, bf16 MFMA (csrc/bb_conv.hip)
+# ---------------------------------------------------------------------------
+_CONV_CH = (64, 128)
+
+
+def conv3x3_fusable(x: torch.Tensor, conv) -> bool:
+    """An nn.Conv2d 3x3 / stride 1 / pad 1 with 64 or 128 channels in and out,
+    applied to a device tensor of 8x8 boards."""
+    return (x.is_cuda and x.dim() == 4 and x.shape[2] == 8 and x.shape[3] == 8 and x.shape[0] > 0
+            and conv.in_channels in _CONV_CH and conv.out_channels in _CONV_CH and conv.groups == 1
+            and tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1)
+            and tuple(conv.padding) == (1, 1) and tuple(conv.dilation) == (1, 1) and conv.padding_mode == "zeros")
+
+
+def _w_layout(w: torch.Tensor) -> int:
+    if w.is_contiguous():
+        return 0
+    if w.is_contiguous(memory_format=torch.channels_last):
+        return 1
+    raise L.BBNativeError("conv weight must be contiguous or channels_last")
+
+
+class Conv3x3Function(torch.autograd.Function):
+    """conv2d(x, weight, padding=1) without bias under bf16 autocast:
+    bf16 NHWC activations, f32 accumulation, bf16 output, f32 weight gradient
+    (bb_conv3x3_prep / _forward / _wgrad; the data gradient is the forward
+    kernel over dy with the tap-reversed, transposed weight image)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        _need_cuda(x, weight)
+        x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        n, cin = x.shape[0], x.shape[1]
+        cout = weight.shape[0]
+        dev = x.device
+        lib = L.load()
+        wl = _w_layout(weight)
+        wf = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
+        wd = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
+        L.check(lib.bb_conv3x3_prep(_p(weight), cin, cout, wl, _p(wf), _p(wd), _s(dev)), "bb_conv3x3_prep")
+        y = torch.empty((n, cout, 8, 8), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+        L.check(lib.bb_conv3x3_forward(_p(x), _p(wf), n, cin, cout, _p(y), _s(dev)), "bb_conv3x3_forward")
+        ctx.save_for_backward(x, wd, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wd, weight = ctx.saved_tensors
+        n, cin = x.shape[0], x.shape[1]
+        cout = weight.shape[0]
+        dev = x.device
+        lib = L.load()
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            L.check(lib.bb_conv3x3_forward(_p(dy), _p(wd), n, cout, cin, _p(dx), _s(dev)), "bb_conv3x3_forward")
+        if ctx.needs_input_grad[1]:
+            nbytes = lib.bb_conv3x3_workspace_bytes(n, cin, cout)
+            if nbytes < 0:
+                raise L.BBNativeError(f"bb_conv3x3_workspace_bytes rejected {n}x{cin}->{cout}")
+            ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+            dw = torch.empty_like(weight, dtype=torch.float32)
+            L.check(lib.bb_conv3x3_wgrad(_p(x), _p(dy), n, cin, cout, _p(ws), _w_layout(dw), _p(dw), _s(dev)),
+                    "bb_conv3x3_wgrad")
+        return dx, dw
+
+
+# ---------------------------------------------------------------------------
 # PPO minibatch loss, forward and backward (csrc/bb_loss.hip)
 # ---------------------------------------------------------------------------
 class PPOLossFunction(torch.autograd.Function):

@@ -311,6 +311,29 @@ int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const flo
                          float entropy_coef, const float* d_grad_loss, float* d_dlogits,
                          float* d_dvalues, void* stream);
 
+/* The CNN's 3x3 / padding-1 convolutions over 8x8 boards (network.py:75-117,
+ * ResidualBlock network.py:14-30; nn.Conv2d.forward and its autograd
+ * backward) under bf16 autocast, for the layers with 64 or 128 channels in and
+ * out.  Activations are bf16 NHWC (channels_last) [N][8][8][C], 16-byte
+ * aligned; accumulation is f32.  bb_conv3x3_prep casts the nn.Conv2d weight
+ * f32 [cout][cin][3][3] (w_layout 0) or [cout][3][3][cin] (w_layout 1, a
+ * channels_last parameter) to bf16 (round to nearest even, as autocast) in two
+ * images: d_wf [9][cout][cin] for the forward and d_wd [9][cin][cout], taps
+ * reversed, for the data gradient.  bb_conv3x3_forward writes
+ * y = conv(x, w) without bias (bf16 [N][8][8][cout]) from d_wf; the data
+ * gradient is the same call on dy with d_wd and cin / cout swapped.
+ * bb_conv3x3_wgrad writes the f32 weight gradient, in w_layout, of
+ * y = conv(x, w) for the output gradient dy; d_ws is caller scratch of
+ * bb_conv3x3_workspace_bytes(N, cin, cout) bytes.  No atomics: results are
+ * deterministic. */
+int64_t bb_conv3x3_workspace_bytes(int32_t N, int32_t cin, int32_t cout);
+int bb_conv3x3_prep(const float* d_w, int32_t cin, int32_t cout, int32_t w_layout, void* d_wf, void* d_wd,
+                    void* stream);
+int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
+                       void* stream);
+int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
+                     int32_t w_layout, float* d_dw, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

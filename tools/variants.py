@@ -15,7 +15,7 @@ from concurrent.futures import ThreadPoolExecutor
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd", "csrc")
 OUT = os.path.join(REPO, "tools", "variants")
-SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_nn.hip", "bb_loss.hip", "bb_capi.cpp", "bb_tables.cpp"]
+SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_nn.hip", "bb_loss.hip", "bb_conv.hip", "bb_capi.cpp", "bb_tables.cpp"]
 
 VARIANTS = {
     # name: extra -D flags on top of the shipped build (runtime/build.py)
@@ -48,6 +48,13 @@ VARIANTS = {
     "mp4": ["-DBB_MULTI_PASSES=4"],
     # pass leaf tests without the line clear (pair_quick_nc): measured -1.3%, not shipped
     "passnc": ["-DBB_PASS_NC=1"],
+    # board convolutions (csrc/bb_conv.hip): forward weight stages (input channels, ring slots);
+    # NOT a correct convolution: 1 = no output stores, 2 = one tap of nine
+    "cf64r2": ["-DBB_CONV_FWD_SCI=64", "-DBB_CONV_FWD_RING=2"],
+    "cf64r3": ["-DBB_CONV_FWD_SCI=64", "-DBB_CONV_FWD_RING=3"],
+    "cf32r3": ["-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
+    "cdiag1": ["-DBB_CONV_DIAG=1"],
+    "cdiag2": ["-DBB_CONV_DIAG=2"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
     "diag3": ["-DBB_ROLL_DIAG=3"],
     # NOT reference semantics (instruction-count attribution only): 1 = in-lane quick test, no wave
