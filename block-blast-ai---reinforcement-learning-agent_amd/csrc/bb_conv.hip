@@ -35,7 +35,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr int kThreads = 256;
-constexpr int kFwdBoards = 2;    // forward: 128 pixel rows per workgroup
+#ifndef BB_CONV_FWD_BOARDS
+#define BB_CONV_FWD_BOARDS 2
+#endif
+// forward: boards (64 pixel rows each) per workgroup; 1 only with 128 output channels
+template <int COUT>
+constexpr int fwd_boards() { return (BB_CONV_FWD_BOARDS == 1 && COUT == 128) ? 1 : 2; }
 constexpr int kWgBoards = 2;     // weight grad: boards per LDS stage
 constexpr int kWgTile = 64;      // weight grad: 64 x 64 (co, ci) tile, all nine taps
 
@@ -147,7 +152,8 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ y, int nb) {
   constexpr int RB = CIN * 2;                 // bytes per pixel row
   constexpr int NCH = CIN / 8;                // 16-byte chunks per pixel row
-  constexpr int ROWS = kFwdBoards * 64;       // 128
+  constexpr int FB = fwd_boards<COUT>();
+  constexpr int ROWS = FB * 64;               // pixel rows
   constexpr int XBYTES = (ROWS + kZeroRows) * RB;
   constexpr int SCI = BB_CONV_FWD_SCI;        // input channels per weight stage (32 or 64)
   constexpr int NCB = CIN / SCI;              // stages per tap
@@ -167,7 +173,7 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
 
   const int tid = threadIdx.x;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int b0 = blockIdx.x * kFwdBoards;
+  const int b0 = blockIdx.x * FB;
 
   // input tile: LDS chunk e = 64 k + lane holds row e / NCH, logical chunk (e % NCH) ^ key(row)
 #pragma unroll
@@ -319,9 +325,14 @@ __global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* 
   __shared__ __attribute__((aligned(16))) uint8_t sm[kWgRing * SBYTES + 4 * 128];
 
   constexpr int TCI = CIN / kWgTile;
-  const int tile = blockIdx.x;
+  constexpr int NT = TCI * (COUT / kWgTile);
+  // XCD-aware order: workgroup ids go round-robin over the 8 XCDs, so the NT tiles of
+  // one chunk (which read the same dy and x slices) get ids 8 apart = the same XCD's L2
+  const int id = blockIdx.x, xcd = id & 7, k8 = id >> 3;
+  const int tile = k8 % NT;
+  const int chunk = (k8 / NT) * 8 + xcd;
+  if (chunk * bpc >= nb) return;  // the whole workgroup: no barrier reached
   const int co_t = (tile / TCI) * kWgTile, ci_t = (tile % TCI) * kWgTile;
-  const int chunk = blockIdx.y;
   const int bb = chunk * bpc;
   const int be = min(nb, bb + bpc);
   const int nst = (be - bb + kWgBoards - 1) / kWgBoards;
@@ -371,34 +382,41 @@ __global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* 
     if (s0 + half < be) {
       const int sdy = (si & (kWgRing - 1)) * SBYTES + half * 64 * 128;
       const int sx = sdy + SROWS * 128;
+      // A (dy^T) fragments of the 4 k-steps: board-local pixels 16ks + 8hh + q (+4)
+      bf16x8 afr[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        // this lane's rows of the two transposed reads: board-local pixels 16ks + 8hh + q (+4), board row 2ks + hh
         const int o0 = 16 * ks + 8 * hh + q;
         const bf16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + sdy + wg_off(o0, ua)));
         const bf16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + sdy + wg_off(o0 + 4, ua)));
-        const bf16x8 afr = __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7);
-        const int yy0 = 2 * ks + hh;
-        auto bload = [&](int t) {
-          const int ddy = t / 3 - 1, ddx = t % 3 - 1;
-          const int iy = yy0 + ddy, ix0 = q + ddx, ix1 = q + 4 + ddx;
-          const bool vy = (unsigned)iy < 8u;
-          const int v0 = iy * 8 + ix0, v1 = iy * 8 + ix1;
-          const int off0 = (vy && (unsigned)ix0 < 8u) ? sx + wg_off(v0, ub) : ZOFF + wg_off(v0 & 3, ub);
-          const int off1 = (vy && (unsigned)ix1 < 8u) ? sx + wg_off(v1, ub) : ZOFF + wg_off(v1 & 3, ub);
-          const bf16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off0));
-          const bf16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off1));
-          return __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
-        };
-        bf16x8 bfr[2];
-        bfr[0] = bload(0);
+        afr[ks] = __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+      // B (shifted x) fragment of input board row u + hh, columns q + dx and q + 4 + dx: tap (dy, dx) of
+      // k-step ks reads u = 2ks + dy, so (ks, +1) and (ks + 1, -1) share one read: 27 reads for 36 MFMAs
+      auto bload = [&](int u, int dx) {
+        const int iy = u + hh, ix0 = q + dx, ix1 = q + 4 + dx;
+        const bool vy = (unsigned)iy < 8u;
+        const int v0 = iy * 8 + ix0, v1 = iy * 8 + ix1;
+        const int off0 = (vy && (unsigned)ix0 < 8u) ? sx + wg_off(v0, ub) : ZOFF + wg_off(v0 & 3, ub);
+        const int off1 = (vy && (unsigned)ix1 < 8u) ? sx + wg_off(v1, ub) : ZOFF + wg_off(v1 & 3, ub);
+        const bf16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off0));
+        const bf16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off1));
+        return __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+      bf16x8 bfr[2];
+      bfr[0] = bload(-1, -1);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          if (t + 1 < 9) bfr[(t + 1) & 1] = bload(t + 1);  // in flight while tap t's MFMA issues
-          __builtin_amdgcn_sched_barrier(0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[t & 1], acc[t], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
+      for (int n = 0; n < 27; ++n) {
+        const int dxi = n / 9, u = n % 9 - 1;
+        if (n + 1 < 27) bfr[(n + 1) & 1] = bload((n + 1) % 9 - 1, (n + 1) / 9 - 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (u & 1) {  // odd u: (ks, dy) = ((u - 1) / 2, +1) and ((u + 1) / 2, -1)
+          if (u >= 1) acc[6 + dxi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[(u - 1) / 2], bfr[n & 1], acc[6 + dxi], 0, 0, 0);
+          if (u <= 5) acc[dxi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[(u + 1) / 2], bfr[n & 1], acc[dxi], 0, 0, 0);
+        } else {      // even u: (u / 2, 0)
+          acc[3 + dxi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[u / 2], bfr[n & 1], acc[3 + dxi], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     // the next stage must have landed (this wave's copies; the barrier covers the others')
@@ -472,7 +490,7 @@ int wgrad_bpc(int nb, int nchunk) {
 
 template <int CIN, int COUT>
 hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s) {
-  hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + kFwdBoards - 1) / kFwdBoards), dim3(kFwdThreads), 0, s,
+  hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>()), dim3(kFwdThreads), 0, s,
                      (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb);
   return hipGetLastError();
 }
@@ -482,7 +500,8 @@ hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, flo
   const int nchunk = wgrad_chunks(nb, CIN, COUT);
   const int bpc = wgrad_bpc(nb, nchunk);
   const int used = (nb + bpc - 1) / bpc;  // chunks that hold boards
-  hipLaunchKernelGGL((conv_wgrad_kernel<CIN, COUT>), dim3((CIN / kWgTile) * (COUT / kWgTile), used), dim3(kWgThreads),
+  const int used8 = (used + 7) / 8 * 8;
+  hipLaunchKernelGGL((conv_wgrad_kernel<CIN, COUT>), dim3((CIN / kWgTile) * (COUT / kWgTile) * used8), dim3(kWgThreads),
                      0, s, (const uint16_t*)x, (const uint16_t*)dy, ws, nb, bpc);
   hipError_t st = hipGetLastError();
   if (st != hipSuccess) return st;

@@ -53,6 +53,9 @@ VARIANTS = {
     "cf64r2": ["-DBB_CONV_FWD_SCI=64", "-DBB_CONV_FWD_RING=2"],
     "cf64r3": ["-DBB_CONV_FWD_SCI=64", "-DBB_CONV_FWD_RING=3"],
     "cf32r3": ["-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
+    "cf32r2": ["-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=2"],
+    "cfb1": ["-DBB_CONV_FWD_BOARDS=1"],
+    "cfb1s32": ["-DBB_CONV_FWD_BOARDS=1", "-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
     "cdiag1": ["-DBB_CONV_DIAG=1"],
     "cdiag2": ["-DBB_CONV_DIAG=2"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
