@@ -356,6 +356,9 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restric
 }
 
 // ---------------------------------------------------------------- launch plan
+#ifndef BB_BN_RBLOCKS
+#define BB_BN_RBLOCKS 512  // NHWC reduction blocks at most
+#endif
 struct Plan {
   int V, cpr, nb;  // vector width, 16-byte chunks per contiguous row, reduction blocks
   dim3 rgrid;      // reduction grid
@@ -371,7 +374,7 @@ Plan plan_for(int esz, int nhwc, int N, int C, int HW) {
     const int rows_per_iter = kBnThreads / p.cpr;
     const int64_t R = (int64_t)N * HW;
     int64_t g = (R + (int64_t)rows_per_iter * 8 - 1) / ((int64_t)rows_per_iter * 8);
-    p.nb = (int)(g < 1 ? 1 : (g > 512 ? 512 : g));  // >= 8 rows per thread
+    p.nb = (int)(g < 1 ? 1 : (g > BB_BN_RBLOCKS ? BB_BN_RBLOCKS : g));  // >= 8 rows per thread
     p.rgrid = dim3(p.nb);
   } else {
     p.cpr = HW / p.V;

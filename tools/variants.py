@@ -57,6 +57,9 @@ VARIANTS = {
     "cfb1": ["-DBB_CONV_FWD_BOARDS=1"],
     "cfb1s32": ["-DBB_CONV_FWD_BOARDS=1", "-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
     "cdiag1": ["-DBB_CONV_DIAG=1"],
+    # BatchNorm NHWC reduction blocks (shipped 512)
+    "bnr1024": ["-DBB_BN_RBLOCKS=1024"],
+    "bnr2048": ["-DBB_BN_RBLOCKS=2048"],
     "cdiag2": ["-DBB_CONV_DIAG=2"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
     "diag3": ["-DBB_ROLL_DIAG=3"],
