@@ -32,6 +32,7 @@ namespace {
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr int kThreads = 256;
@@ -136,6 +137,12 @@ constexpr int kZeroRows = 16;
 #ifndef BB_CONV_FWD_SCI
 #define BB_CONV_FWD_SCI 64
 #endif
+#ifndef BB_CONV_MFMA16
+#define BB_CONV_MFMA16 1  // forward tiles on mfma_f32_16x16x32_bf16 (0: 32x32x16)
+#endif
+#ifndef BB_CONV_WG16
+#define BB_CONV_WG16 0  // 1: weight-gradient tiles on mfma_f32_16x16x32_bf16 (parity-green, 14% slower)
+#endif
 #ifndef BB_CONV_DIAG
 #define BB_CONV_DIAG 0  // diagnostics only: 1 = no output stores, 2 = one tap of the nine
 #endif
@@ -200,6 +207,92 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
   BB_WAIT_VM_LGKM0((DIST - 1) * GPW);  // the input tile and stage 0 have landed
   raw_barrier();
 
+#if BB_CONV_MFMA16
+  // mfma_f32_16x16x32_bf16 tiles (holds a higher clock than 32x32x16 under load, MI355X_MICROARCH.md):
+  // lane l holds A[co0 + 16jn + (l & 15)][k 8(l >> 4) + j], B[k 8(l >> 4) + j][px0 + 16im + (l & 15)],
+  // D[co0 + 16jn + 4(l >> 4) + reg][px0 + 16im + (l & 15)]
+  constexpr int TN16 = 4;                     // 16-co tiles per wave (64 co)
+  constexpr int TM16 = (ROWS / WM) / 16;      // 16-px tiles per wave
+  constexpr int KK16 = SCI / 32;              // k-steps of 32 per stage
+  const int r16 = lane & 15, hq = lane >> 4;
+  const int co0 = (wid % WN) * 64;
+  const int px0 = (wid / WN) * (ROWS / WM);
+  int abase[TN16], akey[TN16];
+#pragma unroll
+  for (int j = 0; j < TN16; ++j) {
+    const int co = co0 + 16 * j + r16;
+    abase[j] = co * SCI * 2;
+    akey[j] = wkey<SCI>(co);
+  }
+  f32x4 acc[TN16][TM16];
+#pragma unroll
+  for (int j = 0; j < TN16; ++j)
+#pragma unroll
+    for (int i = 0; i < TM16; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[j][i][e] = 0.f;
+
+  int rb[TM16], key[TM16];
+  for (int st = 0; st < NS; ++st) {
+    if (st + DIST < NS) stage_w(st + DIST);  // its slot was last read in stage st-1, before the barrier
+    const int cb = st % NCB;
+    if (cb == 0) {
+      const int t = st / NCB, dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < TM16; ++i) {
+        const int px = px0 + 16 * i + r16;
+        const int p = px & 63, yy = (p >> 3) + dy, xc = (p & 7) + dx;
+        const int row = ((unsigned)yy < 8u && (unsigned)xc < 8u) ? (px & ~63) + yy * 8 + xc
+                                                                  : ROWS + ((px + 8 * dy + dx) & 15);
+        rb[i] = row * RB;
+        key[i] = fwd_key<CIN>(row);
+      }
+    }
+    const uint8_t* wb = sm + XBYTES + (st % kFwdRing) * WBYTES;
+    bf16x8 afr[2][TN16], bfr[2][TM16];
+    auto load = [&](int kk, int set) {
+#pragma unroll
+      for (int j = 0; j < TN16; ++j)
+        afr[set][j] = *reinterpret_cast<const bf16x8*>(wb + abase[j] + (((4 * kk + hq) ^ akey[j]) << 4));
+#pragma unroll
+      for (int i = 0; i < TM16; ++i)
+        bfr[set][i] = *reinterpret_cast<const bf16x8*>(xs + rb[i] + (((cb * (SCI / 8) + 4 * kk + hq) ^ key[i]) << 4));
+    };
+    load(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < KK16; ++kk) {
+      if (kk + 1 < KK16) load(kk + 1, (kk + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < TN16; ++j)
+#pragma unroll
+        for (int i = 0; i < TM16; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[kk & 1][j], bfr[kk & 1][i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int after = min(NS, st + DIST + 1) - (st + 2);
+    if (after >= 4) BB_WAIT_VM(4 * GPW);
+    else if (after == 3) BB_WAIT_VM(3 * GPW);
+    else if (after == 2) BB_WAIT_VM(2 * GPW);
+    else if (after == 1) BB_WAIT_VM(GPW);
+    else BB_WAIT_VM(0);
+    raw_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < TM16; ++i) {
+    const int px = px0 + 16 * i + r16;
+    if (b0 + (px >> 6) >= nb) continue;
+    if (BB_CONV_DIAG == 1 && acc[0][i][0] != 1.2345e-30f) continue;
+    uint16_t* yo = y + (size_t(b0) * 64 + px) * COUT + co0 + 4 * hq;
+#pragma unroll
+    for (int j = 0; j < TN16; ++j) {
+      uint2 v;
+      v.x = pack2(acc[j][i][0], acc[j][i][1]);
+      v.y = pack2(acc[j][i][2], acc[j][i][3]);
+      *reinterpret_cast<uint2*>(yo + 16 * j) = v;
+    }
+  }
+#else
   const int r = lane & 31, h = lane >> 5;
   const int co0 = (wid % WN) * 64;
   const int px0 = (wid / WN) * (ROWS / WM);
@@ -286,6 +379,7 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
         *reinterpret_cast<uint2*>(yo + 32 * j + 8 * g) = v;
       }
   }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -363,11 +457,23 @@ __global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* 
   const int ua = wc * 8 + ucol;       // dy unit (co)
   const int ub = wi * 8 + ucol;       // x unit (ci)
 
+#if BB_CONV_WG16
+  // mfma_f32_16x16x32_bf16: k = 32 pixels; lane group g (= lane >> 4) holds k 8g..8g+7, column lane & 15;
+  // tile (jc, ji) of the wave's 32 x 32 is acc[t][2 jc + ji]
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int z = 0; z < 4; ++z)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][z][e] = 0.f;
+#else
   f32x16 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+#endif
 
   const int pre = min(nst, kWgRing - 1);
   for (int si = 0; si < pre; ++si) stage(si);
@@ -382,6 +488,43 @@ __global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* 
     if (s0 + half < be) {
       const int sdy = (si & (kWgRing - 1)) * SBYTES + half * 64 * 128;
       const int sx = sdy + SROWS * 128;
+#if BB_CONV_WG16
+      // A (dy^T) fragments: k-step ks (32 pixels) x co tile jc: pixels 32ks + 8g + q (+4), channels 16jc + 4p..
+      bf16x8 afr[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int jc = 0; jc < 2; ++jc) {
+          const int o0 = 32 * ks + 8 * g + q;
+          const int u = wc * 8 + 4 * jc + p;
+          const bf16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + sdy + wg_off(o0, u)));
+          const bf16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + sdy + wg_off(o0 + 4, u)));
+          afr[ks][jc] = __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      // B (shifted x) fragments of tap t, k-step ks, ci tile ji: input board row 4ks + g + dy, columns q + dx, q + 4 + dx
+      auto bload = [&](int t, int ks, int ji) {
+        const int dy = t / 3 - 1, dx = t % 3 - 1;
+        const int iy = 4 * ks + g + dy, ix0 = q + dx, ix1 = q + 4 + dx;
+        const int u = wi * 8 + 4 * ji + p;
+        const bool vy = (unsigned)iy < 8u;
+        const int v0 = iy * 8 + ix0, v1 = iy * 8 + ix1;
+        const int off0 = (vy && (unsigned)ix0 < 8u) ? sx + wg_off(v0, u) : ZOFF + wg_off(v0 & 3, u);
+        const int off1 = (vy && (unsigned)ix1 < 8u) ? sx + wg_off(v1, u) : ZOFF + wg_off(v1 & 3, u);
+        const bf16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off0));
+        const bf16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(sm + off1));
+        return __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+#pragma unroll
+      for (int n = 0; n < 18; ++n) {  // (tap, k-step) pairs
+        const int t = n >> 1, ks = n & 1;
+        const bf16x8 b0 = bload(t, ks, 0), b1 = bload(t, ks, 1);
+#pragma unroll
+        for (int jc = 0; jc < 2; ++jc) {
+          acc[t][2 * jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[ks][jc], b0, acc[t][2 * jc], 0, 0, 0);
+          acc[t][2 * jc + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[ks][jc], b1, acc[t][2 * jc + 1], 0, 0, 0);
+        }
+      }
+#else
       // A (dy^T) fragments of the 4 k-steps: board-local pixels 16ks + 8hh + q (+4)
       bf16x8 afr[4];
 #pragma unroll
@@ -418,6 +561,7 @@ __global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* 
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+    #endif
     }
     // the next stage must have landed (this wave's copies; the barrier covers the others')
     const int after = min(nst, si + kWgRing) - (si + 2);  // stages issued after stage si+1
@@ -438,7 +582,12 @@ __global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* 
 #pragma unroll
       for (int t = t0; t < t0 + 3; ++t)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) red[((t - t0) * 16 + e) * 256 + slot] = acc[t][e];
+        for (int e = 0; e < 16; ++e)
+#if BB_CONV_WG16
+          red[((t - t0) * 16 + e) * 256 + slot] = acc[t][e >> 2][e & 3];
+#else
+          red[((t - t0) * 16 + e) * 256 + slot] = acc[t][e];
+#endif
     }
     __syncthreads();
     if (half == 0) {
@@ -446,8 +595,15 @@ __global__ void __launch_bounds__(kWgThreads) conv_wgrad_kernel(const uint16_t* 
       for (int t = t0; t < t0 + 3; ++t)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
+#if BB_CONV_WG16
+          // tile z = e >> 2 = 2 jc + ji, register e & 3: co 16 jc + 4g + reg, ci 16 ji + (lane & 15)
+          const int co = co_t + 32 * wc + 16 * (e >> 3) + 4 * g + (e & 3);
+          const int ci = ci_t + 32 * wi + 16 * ((e >> 2) & 1) + (lane & 15);
+          pp[((size_t)t * COUT + co) * CIN + ci] = acc[t][e >> 2][e & 3] + red[((t - t0) * 16 + e) * 256 + slot];
+#else
           const int co = co_t + 32 * wc + (e & 3) + 8 * (e >> 2) + 4 * h;
           pp[((size_t)t * COUT + co) * CIN + ci_t + 32 * wi + r] = acc[t][e] + red[((t - t0) * 16 + e) * 256 + slot];
+#endif
         }
     }
     __syncthreads();

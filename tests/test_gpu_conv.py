@@ -141,3 +141,29 @@ def test_network_bf16_hip_conv_matches_miopen(cuda, lib):
     for name, a, b in rows:
         assert a <= 1.5 * b + 2e-3, f"{name}: HIP bf16 error {a:.4f} vs MIOpen bf16 {b:.4f}\n{table}"
     print(table)
+
+
+def test_network_routes_bf16_convs_to_hip(cuda, lib, monkeypatch):
+    """Under bf16 autocast the six 64/128-channel 3x3 layers of the conv stack
+    run on Conv3x3Function (no silent MIOpen fallback); the 4->64 input layer
+    and f32 runs stay on torch's convolution."""
+    import runtime.kernels as K
+    from models.network import BlockBlastNetwork
+
+    calls = []
+    orig = K.Conv3x3Function.apply
+
+    def counting(x, w):
+        calls.append((x.shape[1], w.shape[0]))
+        return orig(x, w)
+
+    monkeypatch.setattr(K.Conv3x3Function, "apply", counting)
+    net = BlockBlastNetwork().to(cuda).train().to(memory_format=torch.channels_last)
+    x = (torch.rand((64, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+        lo, va = net.raw(x)
+    (lo.float().sum() + va.float().sum()).backward()
+    assert sorted(calls) == sorted([(64, 128)] + [(128, 128)] * 5), calls
+    calls.clear()
+    net.raw(x)  # f32: torch's convolutions
+    assert calls == []
