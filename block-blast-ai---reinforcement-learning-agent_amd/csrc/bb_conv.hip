@@ -140,6 +140,9 @@ constexpr int kZeroRows = 16;
 #ifndef BB_CONV_MFMA16
 #define BB_CONV_MFMA16 1  // forward tiles on mfma_f32_16x16x32_bf16 (0: 32x32x16)
 #endif
+#ifndef BB_CONV_STORE_LDS
+#define BB_CONV_STORE_LDS 1  // forward output staged through LDS for 16-byte coalesced stores
+#endif
 #ifndef BB_CONV_WG16
 #define BB_CONV_WG16 0  // 1: weight-gradient tiles on mfma_f32_16x16x32_bf16 (parity-green, 14% slower)
 #endif
@@ -278,6 +281,32 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
     else BB_WAIT_VM(0);
     raw_barrier();
   }
+#if BB_CONV_STORE_LDS
+  // the output tile goes through LDS (free after the last stage's barrier) so that every global
+  // store is a whole 16-byte chunk of a pixel row: row px of COUT bf16, 16-byte chunk c at c ^ (px & 15)
+  constexpr int OCH = COUT / 8;  // 16-byte chunks per output row
+  uint8_t* const os = sm;
+#pragma unroll
+  for (int i = 0; i < TM16; ++i) {
+    const int px = px0 + 16 * i + r16;
+#pragma unroll
+    for (int j = 0; j < TN16; ++j) {
+      const int co = co0 + 16 * j + 4 * hq;  // 4 channels = half of chunk co / 8
+      uint2 v;
+      v.x = pack2(acc[j][i][0], acc[j][i][1]);
+      v.y = pack2(acc[j][i][2], acc[j][i][3]);
+      *reinterpret_cast<uint2*>(os + px * (COUT * 2) + (((co >> 3) ^ (px & 15 & (OCH - 1))) << 4) + ((co & 4) << 1)) = v;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < ROWS * OCH; e += kFwdThreads) {
+    const int px = e / OCH, c = e % OCH;
+    if (b0 + (px >> 6) >= nb) continue;
+    if (BB_CONV_DIAG == 1 && acc[0][0][0] != 1.2345e-30f) continue;
+    *reinterpret_cast<uint4*>(y + (size_t(b0) * 64 + px) * COUT + c * 8) =
+        *reinterpret_cast<const uint4*>(os + px * (COUT * 2) + ((c ^ (px & 15 & (OCH - 1))) << 4));
+  }
+#else
 #pragma unroll
   for (int i = 0; i < TM16; ++i) {
     const int px = px0 + 16 * i + r16;
@@ -292,6 +321,7 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
       *reinterpret_cast<uint2*>(yo + 16 * j) = v;
     }
   }
+#endif
 #else
   const int r = lane & 31, h = lane >> 5;
   const int co0 = (wid % WN) * 64;

@@ -58,6 +58,7 @@ VARIANTS = {
     "cfb1s32": ["-DBB_CONV_FWD_BOARDS=1", "-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
     "cm32": ["-DBB_CONV_MFMA16=0"],
     "cw16": ["-DBB_CONV_WG16=1"],
+    "cst0": ["-DBB_CONV_STORE_LDS=0"],
     "cdiag1": ["-DBB_CONV_DIAG=1"],
     # BatchNorm NHWC reduction blocks (shipped 512)
     "bnr1024": ["-DBB_BN_RBLOCKS=1024"],
