@@ -57,6 +57,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 
 
 HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs on csrc/bb_conv.hip under bf16
+NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
 
 
 def conv_nobias(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -177,6 +178,20 @@ class BlockBlastNetwork(nn.Module):
     def trunk(self, x: torch.Tensor) -> torch.Tensor:
         """x: (B, 4, 8, 8) -> fc features (B, fc_hidden[-1])."""
         h = self.conv_encoder(x)
+        lin0 = self.fc_encoder[0] if len(self.fc_encoder) else None
+        if (NHWC_FLATTEN and isinstance(lin0, nn.Linear) and h.is_cuda
+                and h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous()):
+            # channels_last activations: flatten in (h, w, c) order (a view, no copy) against the
+            # first FC weight's columns permuted the same way -- the reference's (c, h, w) flatten
+            # (network.py:163) copied 33.5 MB per minibatch forward and left its gradient in the
+            # other layout for the ReLU backward of the last residual block
+            n, c, hh, ww = h.shape
+            o = lin0.out_features
+            w = lin0.weight.view(o, c, hh, ww).permute(0, 2, 3, 1).reshape(o, hh * ww * c)
+            z = F.linear(h.permute(0, 2, 3, 1).reshape(n, hh * ww * c), w, lin0.bias)
+            for m in list(self.fc_encoder)[1:]:
+                z = m(z)
+            return z
         return self.fc_encoder(h.reshape(h.shape[0], -1))
 
     def raw(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -167,3 +167,41 @@ def test_network_routes_bf16_convs_to_hip(cuda, lib, monkeypatch):
     calls.clear()
     net.raw(x)  # f32: torch's convolutions
     assert calls == []
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_nhwc_flatten_matches_reference_flatten(cuda, lib, autocast):
+    """The channels_last trunk flattens in (h, w, c) order against the first FC
+    weight permuted the same way (models/network.py NHWC_FLATTEN): same
+    features and the same parameter gradients as the reference's (c, h, w)
+    flatten (network.py:163), f32 and bf16."""
+    import models.network as NW
+    from models.network import BlockBlastNetwork
+
+    torch.manual_seed(9)
+    net = BlockBlastNetwork().to(cuda).train().to(memory_format=torch.channels_last)
+    for m in net.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    x = (torch.rand((256, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for flat in (True, False):
+        NW.NHWC_FLATTEN = flat
+        net.zero_grad(set_to_none=True)
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False, enabled=autocast):
+                f = net.trunk(x)
+        finally:
+            NW.NHWC_FLATTEN = True
+        f.float().square().sum().backward()
+        outs.append((f.detach().float(), {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}))
+    (fa, ga), (fb, gb) = outs
+    # f32: MIOpen's weight-gradient algorithms accumulate in varying order (split-K with atomics),
+    # so the first layers' gradients move by ~1e-3 between any two runs (see test_gpu_ppo_kernels)
+    tol = 2e-2 if autocast else 5e-3
+    assert float((fa - fb).norm() / fb.norm()) < tol
+    params = dict(net.named_parameters())
+    for k in gb:
+        if k.endswith(".bias") and params[k[:-5] + ".weight"].dim() == 4:
+            continue  # conv biases feed a BatchNorm: true gradient 0, both sides rounding noise
+        assert float((ga[k] - gb[k]).norm() / gb[k].norm()) < tol, k
