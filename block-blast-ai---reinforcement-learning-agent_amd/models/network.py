@@ -187,7 +187,10 @@ class BlockBlastNetwork(nn.Module):
             # other layout for the ReLU backward of the last residual block
             n, c, hh, ww = h.shape
             o = lin0.out_features
-            w = lin0.weight.view(o, c, hh, ww).permute(0, 2, 3, 1).reshape(o, hh * ww * c)
+            wp = lin0.weight.view(o, c, hh, ww).permute(0, 2, 3, 1)
+            if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+                wp = wp.to(torch.bfloat16, memory_format=torch.contiguous_format)  # autocast's cast + the permute, one pass
+            w = wp.reshape(o, hh * ww * c)
             z = F.linear(h.permute(0, 2, 3, 1).reshape(n, hh * ww * c), w, lin0.bias)
             for m in list(self.fc_encoder)[1:]:
                 z = m(z)
