@@ -34,6 +34,7 @@ from runtime import kernels as K
 from .base import BaseAgent
 
 _EPS32 = float(torch.finfo(torch.float32).eps)  # Categorical clamp_probs
+FUSED_ADAM = os.environ.get("BB_FUSED_ADAM", "1") != "0"  # clip_grad_norm_ + Adam on bb_adam_clip_step (GPU)
 
 
 @dataclass
@@ -270,6 +271,7 @@ class PPOAgent(BaseAgent):
         self.use_graphs = self.device.type == "cuda"
         self._graphs = {}
         self.fused_loss = True  # the minibatch loss on bb_ppo_loss_* (GPU tensors only)
+        self._adam_ws = None  # bb_adam_clip_step scratch, keyed by the parameter sizes
 
     # ------------------------------------------------------------ helpers
     def set_channels_last(self, on: bool = True) -> None:
@@ -392,8 +394,50 @@ class PPOAgent(BaseAgent):
             for p in self.network.parameters():
                 p.grad = None
             loss.backward()
-        nn.utils.clip_grad_norm_(self.network.parameters(), self.config.max_grad_norm)
-        self.optimizer.step()
+        if not self._fused_clip_adam():
+            nn.utils.clip_grad_norm_(self.network.parameters(), self.config.max_grad_norm)
+            self.optimizer.step()
+
+    def _fused_clip_adam(self) -> bool:
+        """clip_grad_norm_(max_grad_norm) + Adam.step() (ppo.py:400-401) on
+        bb_adam_clip_step: three launches instead of torch's ~8 (per-tensor norms,
+        scalar ops, a multi-tensor scale, two multi-tensor Adam launches).  Same
+        state tensors as torch's fused Adam (exp_avg, exp_avg_sq, device step),
+        so save / load are unchanged.  False (nothing done) where it does not
+        apply: then the torch path runs."""
+        opt = self.optimizer
+        if not (FUSED_ADAM and self.device.type == "cuda" and type(opt) is torch.optim.Adam
+                and len(opt.param_groups) == 1):
+            return False
+        grp = opt.param_groups[0]
+        if (grp["weight_decay"] != 0 or grp["amsgrad"] or grp["maximize"] or torch.is_tensor(grp["lr"])
+                or grp.get("differentiable")):
+            return False
+        params = [p for p in grp["params"] if p.grad is not None]  # clip and Adam both skip the others
+        if not params or len(params) > K.OPT_MAX_TENSORS:
+            return False
+        for p in params:
+            g = p.grad
+            dense = p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last))
+            if not (p.is_cuda and p.dtype == g.dtype == torch.float32 and dense and g.stride() == p.stride()
+                    and not g.is_sparse):
+                return False
+            st = opt.state[p]
+            if len(st) == 0:  # torch's _init_group for fused / capturable Adam: the step count on the device
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            if not (st["step"].is_cuda and st["step"].dtype == torch.float32
+                    and st["exp_avg"].stride() == p.stride() and st["exp_avg_sq"].stride() == p.stride()):
+                return False
+        key = tuple(p.numel() for p in params)
+        if self._adam_ws is None or self._adam_ws[0] != key:
+            self._adam_ws = (key, K.adam_clip_workspace(list(key), self.device))
+        b1, b2 = grp["betas"]
+        K.adam_clip_step(params, [p.grad for p in params], [opt.state[p]["exp_avg"] for p in params],
+                         [opt.state[p]["exp_avg_sq"] for p in params], [opt.state[p]["step"] for p in params],
+                         grp["lr"], b1, b2, grp["eps"], self.config.max_grad_norm, self._adam_ws[1])
+        return True
 
     def train_minibatch(self, x, masks, actions, old_log_probs, advantages, returns) -> torch.Tensor:
         """One PPO optimizer step on a minibatch (ppo.py:362-401): loss, backward,

@@ -685,3 +685,40 @@ extern "C" int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, in
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_wgrad");
   return BB_OK;
 }
+
+static_assert(BB_OPT_MAX_TENSORS == kOptMaxTensors, "bbvec.h / bb_env_internal.h tensor-table size");
+
+extern "C" int64_t bb_adam_clip_workspace_bytes(int32_t num_tensors, const int64_t* h_numel) {
+  if (num_tensors <= 0 || num_tensors > BB_OPT_MAX_TENSORS || !h_numel) return -1;
+  return adam_clip_workspace_bytes(num_tensors, h_numel);
+}
+
+extern "C" int bb_adam_clip_step(int32_t num_tensors, float* const* h_param, float* const* h_grad,
+                                 float* const* h_exp_avg, float* const* h_exp_avg_sq, float* const* h_step,
+                                 const int64_t* h_numel, double lr, double beta1, double beta2, double eps,
+                                 float max_norm, double* d_ws, float* d_total_norm, void* stream) {
+  if (num_tensors <= 0 || num_tensors > BB_OPT_MAX_TENSORS)
+    return fail(nullptr, BB_ERR_ARG, "bb_adam_clip_step: 1 to BB_OPT_MAX_TENSORS tensors");
+  if (!h_param || !h_grad || !h_exp_avg || !h_exp_avg_sq || !h_step || !h_numel || !d_ws)
+    return fail(nullptr, BB_ERR_ARG, "bb_adam_clip_step: NULL argument");
+  if (!al16(d_ws)) return fail(nullptr, BB_ERR_ARG, "bb_adam_clip_step: d_ws must be 16-byte aligned");
+  hipError_t st = launch_adam_clip(num_tensors, h_param, h_grad, h_exp_avg, h_exp_avg_sq, h_step, h_numel, lr, beta1,
+                                   beta2, eps, max_norm, d_ws, d_total_norm, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_adam_clip_step: empty tensor or NULL tensor pointer");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_adam_clip_step");
+  return BB_OK;
+}
+
+extern "C" int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const* h_src, void* const* h_dst,
+                             const int64_t* h_numel, const int32_t* h_perm_c, const int32_t* h_perm_hw, void* stream) {
+  if (num_tensors <= 0 || num_tensors > BB_OPT_MAX_TENSORS)
+    return fail(nullptr, BB_ERR_ARG, "bb_cast_multi: 1 to BB_OPT_MAX_TENSORS tensors");
+  if (dir != 0 && dir != 1) return fail(nullptr, BB_ERR_ARG, "bb_cast_multi: dir must be 0 (f32->bf16) or 1");
+  if (!h_src || !h_dst || !h_numel) return fail(nullptr, BB_ERR_ARG, "bb_cast_multi: NULL argument");
+  hipError_t st = launch_cast_multi(num_tensors, dir, h_src, h_dst, h_numel, h_perm_c, h_perm_hw, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_cast_multi: empty tensor, NULL pointer or bad permutation");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_cast_multi");
+  return BB_OK;
+}

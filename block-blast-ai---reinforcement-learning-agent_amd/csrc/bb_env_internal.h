@@ -117,6 +117,14 @@ hipError_t launch_ppo_loss_backward(const float* logits, const float* values, co
                                     int B, float clip, float vcoef, float ecoef, const float* gloss, float* dlogits,
                                     float* dvalues, hipStream_t s);
 
+constexpr int kOptMaxTensors = 48;  // == BB_OPT_MAX_TENSORS
+int64_t adam_clip_workspace_bytes(int count, const int64_t* n);
+hipError_t launch_adam_clip(int count, float* const* p, float* const* g, float* const* m, float* const* v,
+                            float* const* step, const int64_t* n, double lr, double beta1, double beta2, double eps,
+                            float max_norm, double* ws, float* norm_out, hipStream_t s);
+hipError_t launch_cast_multi(int count, int dir, const void* const* src, void* const* dst, const int64_t* n,
+                             const int32_t* perm_c, const int32_t* perm_hw, hipStream_t s);
+
 // Host helpers (bb_tables.cpp).
 void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces]);
 void build_jump_table(JumpRow rows[kJumpMax + 1]);

@@ -1,0 +1,337 @@
+// bb_optim.hip -- the tail of the PPO minibatch step (gfx950): gradient-norm
+// clipping + Adam in three launches, and the CNN's autocast weight casts of the
+// Linear layers in one launch each way.
+//
+// PPOAgent.update (ppo.py:400-401) runs nn.utils.clip_grad_norm_(params, 0.5)
+// and torch.optim.Adam(lr, eps=1e-5).step() after every minibatch backward.
+// torch issues them as a per-tensor norm kernel, a few scalar kernels, a
+// multi-tensor scale and two multi-tensor Adam launches (~115 us per step at
+// 5.29 M parameters, ~2 TB/s); here they are
+//   adam_norm_kernel     : sum of g^2 per chunk of 2,048 elements -> fp64 partials
+//   adam_finalize_kernel : one workgroup adds the partials in a fixed order
+//                          (deterministic), clip coefficient
+//                          min(max_norm / (||g|| + 1e-6), 1), step += 1 per
+//                          tensor, Adam's bias corrections;
+//   adam_update_kernel   : g *= coef (written back, as clip_grad_norm_ leaves
+//                          it), then torch's fused Adam arithmetic
+//                          (fused_adam_utils.cuh adam_math, ADAM_MODE::ORIGINAL:
+//                          the moment updates in double, step size lr / bc1,
+//                          denom sqrt(v) / sqrt(bc2) + eps).
+// Every kernel is one HBM pass over its operands; the tensor table travels in
+// the kernel arguments, so a HIP graph can capture the launches.
+//
+// Casts: under bf16 autocast every nn.Linear of the CNN casts its f32 weight
+// and bias to bf16 in a kernel of its own, and autograd casts the bf16 weight
+// gradients back (24 launches per step, plus a strided permute-copy of the
+// first FC weight for the channels_last flatten, network.py trunk).
+// cast_multi_kernel does all tensors of one direction in one launch; a tensor
+// with perm_c > 0 is [O][perm_c][perm_hw] on the f32 side and [O][perm_hw][perm_c]
+// on the bf16 side (transposed per row through LDS, both sides coalesced).
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <math.h>
+
+#include "bb_env_internal.h"
+
+namespace bb {
+
+namespace {
+
+constexpr int kOptThreads = 256;
+constexpr int kOptChunk = 2048;  // elements per workgroup (8 per thread)
+constexpr int kCastChunk = 8192; // elements per workgroup in the casts (one permuted row at most)
+
+struct AdamTable {
+  float* p[kOptMaxTensors];
+  float* g[kOptMaxTensors];
+  float* m[kOptMaxTensors];
+  float* v[kOptMaxTensors];
+  float* step[kOptMaxTensors];
+  int64_t n[kOptMaxTensors];
+  int32_t chunk0[kOptMaxTensors + 1];  // first chunk of tensor t; chunk0[count] = total
+  int32_t count;
+};
+
+struct CastTable {
+  const void* src[kOptMaxTensors];
+  void* dst[kOptMaxTensors];
+  int64_t n[kOptMaxTensors];
+  int32_t perm_c[kOptMaxTensors];
+  int32_t perm_hw[kOptMaxTensors];
+  int32_t chunk0[kOptMaxTensors + 1];
+  int32_t count;
+};
+
+// workspace: [0, kHdr) doubles of header (coef, norm, per-tensor bc1 / sqrt(bc2) as floats), then partials
+constexpr int kHdr = 8 + kOptMaxTensors;
+
+template <typename Tab>
+__device__ __forceinline__ int find_tensor(const Tab& tab, int chunk) {
+  int t = 0;
+  while (t + 1 < tab.count && tab.chunk0[t + 1] <= chunk) ++t;  // uniform scan over <= 48 kernel arguments
+  return t;
+}
+
+__device__ double block_sum(double x, double* red) {
+  // fixed-order tree over the workgroup (deterministic)
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = x;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < kOptThreads / 64; ++i) s += red[i];
+  return s;
+}
+
+__global__ void __launch_bounds__(kOptThreads) adam_norm_kernel(const AdamTable tab, double* __restrict__ ws) {
+  __shared__ double red[kOptThreads / 64];
+  const int chunk = blockIdx.x;
+  const int t = find_tensor(tab, chunk);
+  const int64_t base = int64_t(chunk - tab.chunk0[t]) * kOptChunk;
+  const int64_t n = tab.n[t];
+  const float* g = tab.g[t];
+  float acc = 0.f;
+  const int64_t i0 = base + threadIdx.x * 4;
+  if (((reinterpret_cast<uintptr_t>(g) & 15) == 0) && base + kOptChunk <= n) {
+    for (int k = 0; k < kOptChunk; k += kOptThreads * 4) {
+      const float4 q = *reinterpret_cast<const float4*>(g + i0 + k);
+      acc += q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+    }
+  } else {
+    for (int64_t i = base + threadIdx.x; i < n && i < base + kOptChunk; i += kOptThreads) acc += g[i] * g[i];
+  }
+  const double s = block_sum(double(acc), red);
+  if (threadIdx.x == 0) ws[kHdr + chunk] = s;
+}
+
+__global__ void __launch_bounds__(kOptThreads) adam_finalize_kernel(const AdamTable tab, double* __restrict__ ws,
+                                                                    float max_norm, double beta1, double beta2,
+                                                                    float* __restrict__ norm_out) {
+  __shared__ double red[kOptThreads / 64];
+  const int nchunks = tab.chunk0[tab.count];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nchunks; i += kOptThreads) s += ws[kHdr + i];
+  s = block_sum(s, red);
+  float* hdr = reinterpret_cast<float*>(ws);
+  if (threadIdx.x == 0) {
+    // clip_grad_norm_: total_norm (f32), clip_coef = max_norm / (total_norm + 1e-6), clamped to <= 1
+    const float norm = float(sqrt(s));
+    const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);
+    hdr[0] = coef;
+    hdr[1] = norm;
+    if (norm_out) *norm_out = norm;
+  }
+  if (threadIdx.x < tab.count) {
+    // torch's fused Adam: state_steps += 1, then the bias corrections from the new step
+    const int t = threadIdx.x;
+    const float st = *tab.step[t] + 1.0f;
+    *tab.step[t] = st;
+    const double bc1 = 1.0 - pow(beta1, double(st));
+    const double bc2 = 1.0 - pow(beta2, double(st));
+    hdr[16 + 2 * t] = float(bc1);
+    hdr[16 + 2 * t + 1] = float(sqrt(bc2));
+  }
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float& g, float& m, float& v, float coef, double lr, double beta1,
+                                          double beta2, double eps, float bc1, float bc2s) {
+  g = g * coef;
+  m = float(beta1 * double(m) + (1.0 - beta1) * double(g));
+  v = float(beta2 * double(v) + (1.0 - beta2) * double(g) * double(g));
+  const float step_size = float(lr / double(bc1));
+  const float denom = float(double(sqrtf(v) / bc2s) + eps);
+  p -= step_size * m / denom;
+}
+
+__global__ void __launch_bounds__(kOptThreads) adam_update_kernel(const AdamTable tab, const double* __restrict__ ws,
+                                                                  double lr, double beta1, double beta2, double eps) {
+  const int chunk = blockIdx.x;
+  const int t = find_tensor(tab, chunk);
+  const int64_t base = int64_t(chunk - tab.chunk0[t]) * kOptChunk;
+  const int64_t n = tab.n[t];
+  const float* hdr = reinterpret_cast<const float*>(ws);
+  const float coef = hdr[0], bc1 = hdr[16 + 2 * t], bc2s = hdr[16 + 2 * t + 1];
+  float *P = tab.p[t], *G = tab.g[t], *M = tab.m[t], *V = tab.v[t];
+  const bool vec = ((reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(M) |
+                     reinterpret_cast<uintptr_t>(V)) & 15) == 0;
+  if (vec && base + kOptChunk <= n) {
+#pragma unroll
+    for (int k = 0; k < kOptChunk; k += kOptThreads * 4) {
+      const int64_t i = base + k + threadIdx.x * 4;
+      float4 p = *reinterpret_cast<float4*>(P + i), g = *reinterpret_cast<float4*>(G + i);
+      float4 m = *reinterpret_cast<float4*>(M + i), v = *reinterpret_cast<float4*>(V + i);
+      adam_elem(p.x, g.x, m.x, v.x, coef, lr, beta1, beta2, eps, bc1, bc2s);
+      adam_elem(p.y, g.y, m.y, v.y, coef, lr, beta1, beta2, eps, bc1, bc2s);
+      adam_elem(p.z, g.z, m.z, v.z, coef, lr, beta1, beta2, eps, bc1, bc2s);
+      adam_elem(p.w, g.w, m.w, v.w, coef, lr, beta1, beta2, eps, bc1, bc2s);
+      *reinterpret_cast<float4*>(P + i) = p;
+      *reinterpret_cast<float4*>(G + i) = g;
+      *reinterpret_cast<float4*>(M + i) = m;
+      *reinterpret_cast<float4*>(V + i) = v;
+    }
+  } else {
+    for (int64_t i = base + threadIdx.x; i < n && i < base + kOptChunk; i += kOptThreads) {
+      float p = P[i], g = G[i], m = M[i], v = V[i];
+      adam_elem(p, g, m, v, coef, lr, beta1, beta2, eps, bc1, bc2s);
+      P[i] = p;
+      G[i] = g;
+      M[i] = m;
+      V[i] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ uint16_t f2bf_rne(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);  // round to nearest even, as autocast's cast
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+
+// DIR 0: f32 -> bf16, DIR 1: bf16 -> f32
+template <int DIR>
+__global__ void __launch_bounds__(kOptThreads) cast_multi_kernel(const CastTable tab) {
+  __shared__ float tile[kCastChunk + kCastChunk / 64];  // one permuted row, padded every 64 floats
+  const int chunk = blockIdx.x;
+  const int t = find_tensor(tab, chunk);
+  const int pc = tab.perm_c[t];
+  const int64_t n = tab.n[t];
+  if (pc > 0) {  // one row [perm_c][perm_hw] (f32 side) <-> [perm_hw][perm_c] (bf16 side) per workgroup
+    const int hw = tab.perm_hw[t], row = pc * hw;
+    const int64_t base = int64_t(chunk - tab.chunk0[t]) * row;
+    auto pad = [](int i) { return i + (i >> 6); };
+    if (DIR == 0) {
+      const float* s = static_cast<const float*>(tab.src[t]) + base;
+      uint16_t* d = static_cast<uint16_t*>(tab.dst[t]) + base;
+      for (int i = threadIdx.x; i < row; i += kOptThreads) tile[pad(i)] = s[i];  // i = c * hw + q
+      __syncthreads();
+      for (int j = threadIdx.x; j < row; j += kOptThreads) {  // j = q * pc + c
+        const int q = j / pc, c = j - q * pc;
+        d[j] = f2bf_rne(tile[pad(c * hw + q)]);
+      }
+    } else {
+      const uint16_t* s = static_cast<const uint16_t*>(tab.src[t]) + base;
+      float* d = static_cast<float*>(tab.dst[t]) + base;
+      for (int j = threadIdx.x; j < row; j += kOptThreads) tile[pad(j)] = bf2f(s[j]);  // j = q * pc + c
+      __syncthreads();
+      for (int i = threadIdx.x; i < row; i += kOptThreads) {  // i = c * hw + q
+        const int c = i / hw, q = i - c * hw;
+        d[i] = tile[pad(q * pc + c)];
+      }
+    }
+    return;
+  }
+  const int64_t base = int64_t(chunk - tab.chunk0[t]) * kCastChunk;
+  const int64_t end = base + kCastChunk < n ? base + kCastChunk : n;
+  if (DIR == 0) {
+    const float* s = static_cast<const float*>(tab.src[t]);
+    uint16_t* d = static_cast<uint16_t*>(tab.dst[t]);
+    const bool vec = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0;
+    int64_t i = base + threadIdx.x * 8;
+    if (vec)
+      for (; i + 8 <= end; i += kOptThreads * 8) {
+        const float4 a = *reinterpret_cast<const float4*>(s + i), b = *reinterpret_cast<const float4*>(s + i + 4);
+        uint4 o;
+        o.x = uint32_t(f2bf_rne(a.x)) | (uint32_t(f2bf_rne(a.y)) << 16);
+        o.y = uint32_t(f2bf_rne(a.z)) | (uint32_t(f2bf_rne(a.w)) << 16);
+        o.z = uint32_t(f2bf_rne(b.x)) | (uint32_t(f2bf_rne(b.y)) << 16);
+        o.w = uint32_t(f2bf_rne(b.z)) | (uint32_t(f2bf_rne(b.w)) << 16);
+        *reinterpret_cast<uint4*>(d + i) = o;
+      }
+    // scalar tail (or the whole chunk when unaligned)
+    const int64_t tail0 = vec ? base + ((end - base) / 8) * 8 : base;
+    for (int64_t k = tail0 + threadIdx.x; k < end; k += kOptThreads) d[k] = f2bf_rne(s[k]);
+  } else {
+    const uint16_t* s = static_cast<const uint16_t*>(tab.src[t]);
+    float* d = static_cast<float*>(tab.dst[t]);
+    const bool vec = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0;
+    if (vec)
+      for (int64_t i = base + threadIdx.x * 8; i + 8 <= end; i += kOptThreads * 8) {
+        const uint4 h = *reinterpret_cast<const uint4*>(s + i);
+        *reinterpret_cast<float4*>(d + i) = make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u),
+                                                        __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xffff0000u));
+        *reinterpret_cast<float4*>(d + i + 4) = make_float4(__uint_as_float(h.z << 16),
+                                                            __uint_as_float(h.z & 0xffff0000u),
+                                                            __uint_as_float(h.w << 16),
+                                                            __uint_as_float(h.w & 0xffff0000u));
+      }
+    const int64_t tail0 = vec ? base + ((end - base) / 8) * 8 : base;
+    for (int64_t k = tail0 + threadIdx.x; k < end; k += kOptThreads) d[k] = bf2f(s[k]);
+  }
+}
+
+int build_adam_table(AdamTable& tab, int count, float* const* p, float* const* g, float* const* m, float* const* v,
+                     float* const* step, const int64_t* n) {
+  if (count <= 0 || count > kOptMaxTensors) return -1;
+  tab.count = count;
+  int64_t c = 0;
+  for (int t = 0; t < count; ++t) {
+    if (n[t] <= 0 || !p[t] || !g[t] || !m[t] || !v[t] || !step[t]) return -1;
+    tab.p[t] = p[t];
+    tab.g[t] = g[t];
+    tab.m[t] = m[t];
+    tab.v[t] = v[t];
+    tab.step[t] = step[t];
+    tab.n[t] = n[t];
+    tab.chunk0[t] = int32_t(c);
+    c += (n[t] + kOptChunk - 1) / kOptChunk;
+    if (c > (1 << 30)) return -1;
+  }
+  tab.chunk0[count] = int32_t(c);
+  return int(c);
+}
+
+}  // namespace
+
+int64_t adam_clip_workspace_bytes(int count, const int64_t* n) {
+  if (count <= 0 || count > kOptMaxTensors) return -1;
+  int64_t c = 0;
+  for (int t = 0; t < count; ++t) {
+    if (n[t] <= 0) return -1;
+    c += (n[t] + kOptChunk - 1) / kOptChunk;
+  }
+  return (kHdr + c) * int64_t(sizeof(double));
+}
+
+hipError_t launch_adam_clip(int count, float* const* p, float* const* g, float* const* m, float* const* v,
+                            float* const* step, const int64_t* n, double lr, double beta1, double beta2, double eps,
+                            float max_norm, double* ws, float* norm_out, hipStream_t s) {
+  AdamTable tab;
+  const int chunks = build_adam_table(tab, count, p, g, m, v, step, n);
+  if (chunks <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(adam_norm_kernel, dim3(chunks), dim3(kOptThreads), 0, s, tab, ws);
+  hipLaunchKernelGGL(adam_finalize_kernel, dim3(1), dim3(kOptThreads), 0, s, tab, ws, max_norm, beta1, beta2,
+                     norm_out);
+  hipLaunchKernelGGL(adam_update_kernel, dim3(chunks), dim3(kOptThreads), 0, s, tab, ws, lr, beta1, beta2, eps);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_multi(int count, int dir, const void* const* src, void* const* dst, const int64_t* n,
+                             const int32_t* perm_c, const int32_t* perm_hw, hipStream_t s) {
+  if (count <= 0 || count > kOptMaxTensors || (dir != 0 && dir != 1)) return hipErrorInvalidValue;
+  CastTable tab;
+  tab.count = count;
+  int64_t c = 0;
+  for (int t = 0; t < count; ++t) {
+    const int pc = perm_c ? perm_c[t] : 0, ph = perm_hw ? perm_hw[t] : 0;
+    if (n[t] <= 0 || !src[t] || !dst[t] || pc < 0) return hipErrorInvalidValue;
+    if (pc > 0 && (ph <= 0 || int64_t(pc) * ph > kCastChunk || n[t] % (int64_t(pc) * ph) != 0))
+      return hipErrorInvalidValue;
+    tab.src[t] = src[t];
+    tab.dst[t] = dst[t];
+    tab.n[t] = n[t];
+    tab.perm_c[t] = pc;
+    tab.perm_hw[t] = pc > 0 ? ph : 0;
+    tab.chunk0[t] = int32_t(c);
+    c += pc > 0 ? n[t] / (int64_t(pc) * ph) : (n[t] + kCastChunk - 1) / kCastChunk;
+    if (c > (1 << 30)) return hipErrorInvalidValue;
+  }
+  tab.chunk0[count] = int32_t(c);
+  if (dir == 0)
+    hipLaunchKernelGGL(cast_multi_kernel<0>, dim3(c), dim3(kOptThreads), 0, s, tab);
+  else
+    hipLaunchKernelGGL(cast_multi_kernel<1>, dim3(c), dim3(kOptThreads), 0, s, tab);
+  return hipGetLastError();
+}
+
+}  // namespace bb

@@ -58,6 +58,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 
 HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs on csrc/bb_conv.hip under bf16
 NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
+FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"  # bf16 Linear weights/biases cast in one launch each way
 
 
 def conv_nobias(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -175,8 +176,50 @@ class BlockBlastNetwork(nn.Module):
                 nn.init.zeros_(m.bias)
 
     # ------------------------------------------------------------------ core
-    def trunk(self, x: torch.Tensor) -> torch.Tensor:
-        """x: (B, 4, 8, 8) -> fc features (B, fc_hidden[-1])."""
+    def _linears(self):
+        return [m for seq in (self.fc_encoder, self.policy_head, self.value_head) for m in seq
+                if isinstance(m, nn.Linear)]
+
+    def _linear_shadows(self, h: torch.Tensor, perm0: Optional[Tuple[int, int]]):
+        """Under bf16 autocast on the GPU: bf16 copies of every Linear weight and
+        bias from one launch (runtime.kernels.LinearCastFunction; autocast
+        otherwise casts them one kernel each, and their gradients back one kernel
+        each).  perm0 = (c, hw): the first FC weight's columns in (hw, c) order
+        for the channels_last flatten.  None when not applicable."""
+        if not (FUSED_CASTS and h.is_cuda and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            return None
+        lins = self._linears()
+        params, perms, slots = [], [], []
+        for m in lins:
+            perm = perm0 if (perm0 is not None and len(self.fc_encoder) and m is self.fc_encoder[0]) else (0, 0)
+            params.append(m.weight)
+            perms.append(perm)
+            if m.bias is not None:
+                params.append(m.bias)
+                perms.append((0, 0))
+            slots.append(m.bias is not None)
+        if not params or len(params) > 48 or any(p.dtype != torch.float32 or not p.is_contiguous() for p in params):
+            return None
+        from runtime.kernels import LinearCastFunction
+
+        outs = list(LinearCastFunction.apply(tuple(perms), *params))
+        sh, k = {}, 0
+        for m, has_b in zip(lins, slots):
+            sh[m] = (outs[k], outs[k + 1] if has_b else None)
+            k += 2 if has_b else 1
+        return sh
+
+    @staticmethod
+    def _run(seq: nn.Sequential, z: torch.Tensor, sh, skip_first: bool = False) -> torch.Tensor:
+        for i, m in enumerate(seq):
+            if skip_first and i == 0:
+                continue
+            z = F.linear(z, *sh[m]) if (sh is not None and isinstance(m, nn.Linear)) else m(z)
+        return z
+
+    def _trunk(self, x: torch.Tensor):
+        """x: (B, 4, 8, 8) -> (fc features (B, fc_hidden[-1]), Linear shadows or None)."""
         h = self.conv_encoder(x)
         lin0 = self.fc_encoder[0] if len(self.fc_encoder) else None
         if (NHWC_FLATTEN and isinstance(lin0, nn.Linear) and h.is_cuda
@@ -187,20 +230,26 @@ class BlockBlastNetwork(nn.Module):
             # other layout for the ReLU backward of the last residual block
             n, c, hh, ww = h.shape
             o = lin0.out_features
+            flat = h.permute(0, 2, 3, 1).reshape(n, hh * ww * c)
+            sh = self._linear_shadows(h, (c, hh * ww))
+            if sh is not None:  # the permuted bf16 weight comes out of the multi-tensor cast
+                return self._run(self.fc_encoder, F.linear(flat, *sh[lin0]), sh, skip_first=True), sh
             wp = lin0.weight.view(o, c, hh, ww).permute(0, 2, 3, 1)
             if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
                 wp = wp.to(torch.bfloat16, memory_format=torch.contiguous_format)  # autocast's cast + the permute, one pass
             w = wp.reshape(o, hh * ww * c)
-            z = F.linear(h.permute(0, 2, 3, 1).reshape(n, hh * ww * c), w, lin0.bias)
-            for m in list(self.fc_encoder)[1:]:
-                z = m(z)
-            return z
-        return self.fc_encoder(h.reshape(h.shape[0], -1))
+            return self._run(self.fc_encoder, F.linear(flat, w, lin0.bias), None, skip_first=True), None
+        sh = self._linear_shadows(h, None)
+        return self._run(self.fc_encoder, h.reshape(h.shape[0], -1), sh), sh
+
+    def trunk(self, x: torch.Tensor) -> torch.Tensor:
+        """x: (B, 4, 8, 8) -> fc features (B, fc_hidden[-1])."""
+        return self._trunk(x)[0]
 
     def raw(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Unmasked logits (B, 192) and value (B,) from the stacked input."""
-        h = self.trunk(x)
-        return self.policy_head(h), self.value_head(h).squeeze(-1)
+        h, sh = self._trunk(x)
+        return self._run(self.policy_head, h, sh), self._run(self.value_head, h, sh).squeeze(-1)
 
     @staticmethod
     def stack_input(board: torch.Tensor, pieces: torch.Tensor) -> torch.Tensor:

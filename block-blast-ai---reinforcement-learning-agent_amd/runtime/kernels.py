@@ -310,3 +310,80 @@ class PPOLossFunction(torch.autograd.Function):
                                               _s(dev)),
                 "bb_ppo_loss_backward")
         return dlogits, dvalues, None, None, None, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------------
+# clip_grad_norm_ + Adam, and the Linear layers' autocast casts (csrc/bb_optim.hip)
+# ---------------------------------------------------------------------------
+OPT_MAX_TENSORS = 48  # BB_OPT_MAX_TENSORS
+
+
+def _ptrs(ts):
+    return (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+def adam_clip_workspace(numels, device) -> torch.Tensor:
+    n = (C.c_int64 * len(numels))(*numels)
+    nbytes = L.load().bb_adam_clip_workspace_bytes(len(numels), n)
+    if nbytes < 0:
+        raise L.BBNativeError(f"bb_adam_clip_workspace_bytes rejected {len(numels)} tensors")
+    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+
+
+def adam_clip_step(params, grads, exp_avgs, exp_avg_sqs, steps, lr: float, beta1: float, beta2: float, eps: float,
+                   max_norm: float, ws: torch.Tensor, total_norm: Optional[torch.Tensor] = None) -> None:
+    """nn.utils.clip_grad_norm_(params, max_norm) + torch.optim.Adam.step()
+    (weight decay 0) in three launches (bb_adam_clip_step): gradients are
+    clipped in place, parameters / moments / step counts updated in place."""
+    k = len(params)
+    if not (len(grads) == len(exp_avgs) == len(exp_avg_sqs) == len(steps) == k) or not 0 < k <= OPT_MAX_TENSORS:
+        raise L.BBNativeError(f"adam_clip_step: 1..{OPT_MAX_TENSORS} tensors with all four states")
+    for p, g, m, v, s in zip(params, grads, exp_avgs, exp_avg_sqs, steps):
+        _need_cuda(p, g, m, v, s)
+        if not (p.dtype == g.dtype == m.dtype == v.dtype == s.dtype == torch.float32):
+            raise L.BBNativeError("adam_clip_step: f32 tensors only")
+        dense = p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last))
+        if not (dense and p.shape == g.shape and p.stride() == g.stride() == m.stride() == v.stride()):
+            raise L.BBNativeError("adam_clip_step: parameter, gradient and moments must share one dense layout")
+    numel = (C.c_int64 * k)(*[p.numel() for p in params])
+    dev = params[0].device
+    L.check(L.load().bb_adam_clip_step(k, _ptrs(params), _ptrs(grads), _ptrs(exp_avgs), _ptrs(exp_avg_sqs),
+                                       _ptrs(steps), numel, float(lr), float(beta1), float(beta2), float(eps),
+                                       float(max_norm), _p(ws), _p(total_norm), _s(dev)),
+            "bb_adam_clip_step")
+
+
+def cast_multi(dir_: int, srcs, dsts, perms) -> None:
+    """bb_cast_multi: dir 0 f32 -> bf16, 1 bf16 -> f32, all tensors in one launch."""
+    k = len(srcs)
+    numel = (C.c_int64 * k)(*[t.numel() for t in srcs])
+    pc = (C.c_int32 * k)(*[p[0] for p in perms])
+    ph = (C.c_int32 * k)(*[p[1] for p in perms])
+    L.check(L.load().bb_cast_multi(k, int(dir_), _ptrs(srcs), _ptrs(dsts), numel, pc, ph, _s(srcs[0].device)),
+            "bb_cast_multi")
+
+
+class LinearCastFunction(torch.autograd.Function):
+    """autocast's f32 -> bf16 casts of the CNN's Linear weights and biases, all
+    in one launch, and the bf16 -> f32 casts of their gradients in one launch
+    (values identical to autocast's per-tensor casts).  perms[i] = (c, hw)
+    stores parameter i's columns, read as [c][hw], in [hw][c] order (the first
+    FC weight against the channels_last flatten); (0, 0) = as is."""
+
+    @staticmethod
+    def forward(ctx, perms, *params):
+        _need_cuda(*params)
+        for p in params:
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise L.BBNativeError("LinearCastFunction: contiguous f32 parameters only")
+        outs = [torch.empty(p.shape, dtype=torch.bfloat16, device=p.device) for p in params]
+        cast_multi(0, params, outs, perms)
+        ctx.perms = perms
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        gin = [g.to(torch.bfloat16).contiguous() for g in grads]
+        outs = [torch.empty(g.shape, dtype=torch.float32, device=g.device) for g in gin]
+        cast_multi(1, gin, outs, ctx.perms)
+        return (None, *outs)

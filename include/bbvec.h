@@ -334,6 +334,35 @@ int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin,
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
 
+/* The end of the PPO minibatch step (PPOAgent.update, ppo.py:400-401):
+ * nn.utils.clip_grad_norm_(params, max_norm) followed by
+ * torch.optim.Adam(lr, betas, eps).step() (weight decay 0, no amsgrad), over
+ * up to BB_OPT_MAX_TENSORS f32 parameter tensors given as host arrays of device
+ * pointers: parameter, gradient, exp_avg, exp_avg_sq (same layout and numel
+ * each) and Adam's per-tensor step count (f32 scalar on the device, incremented
+ * first, as torch's fused / capturable Adam keeps it).  The gradient is scaled
+ * by min(max_norm / (||g||_2 + 1e-6), 1) in place, as clip_grad_norm_ leaves
+ * it; ||g|| over all tensors is written to d_total_norm when non-NULL.  d_ws is
+ * caller scratch of bb_adam_clip_workspace_bytes(num_tensors, h_numel) bytes
+ * (16-byte aligned).  Three kernel launches on `stream`; the tensor table is
+ * passed by value, so the launches can be captured into a HIP graph.  The norm
+ * is summed in a fixed order: deterministic. */
+#define BB_OPT_MAX_TENSORS 48
+int64_t bb_adam_clip_workspace_bytes(int32_t num_tensors, const int64_t* h_numel);
+int bb_adam_clip_step(int32_t num_tensors, float* const* h_param, float* const* h_grad,
+                      float* const* h_exp_avg, float* const* h_exp_avg_sq, float* const* h_step,
+                      const int64_t* h_numel, double lr, double beta1, double beta2, double eps,
+                      float max_norm, double* d_ws, float* d_total_norm, void* stream);
+
+/* bf16 autocast's parameter casts for the CNN's nn.Linear layers
+ * (network.py:89-117 under torch.autocast), all tensors in one launch: dir 0
+ * casts f32 -> bf16 (round to nearest even), dir 1 bf16 -> f32 (their
+ * gradients).  h_perm_c (NULL = none) > 0 marks a tensor of O rows whose f32
+ * side is [O][perm_c][perm_hw] and whose bf16 side is [O][perm_hw][perm_c] (the
+ * first FC weight against a channels_last flatten); perm_c * perm_hw <= 8192. */
+int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const* h_src, void* const* h_dst,
+                  const int64_t* h_numel, const int32_t* h_perm_c, const int32_t* h_perm_hw, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
