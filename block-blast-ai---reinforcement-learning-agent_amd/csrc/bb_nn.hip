@@ -32,8 +32,14 @@ namespace {
 
 constexpr int kBnThreads = 256;
 // rows in flight per thread in the NHWC reductions (forward: one tensor; backward: x and dy)
+#ifndef BB_BN_UNROLL_BWD
+#define BB_BN_UNROLL_BWD 2  // 2: -0.5% on the update step against 4 (8: +0.5%), profiles/r02/optim/bnab_*
+#endif
+#ifndef BB_BN_UNROLL_FWD
+#define BB_BN_UNROLL_FWD 8
+#endif
 template <bool BWD>
-constexpr int kUnroll = BWD ? 4 : 8;
+constexpr int kUnroll = BWD ? BB_BN_UNROLL_BWD : BB_BN_UNROLL_FWD;
 constexpr int kQ = 3;       // partial quantities per channel
 
 template <typename T>

@@ -15,7 +15,8 @@ from concurrent.futures import ThreadPoolExecutor
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd", "csrc")
 OUT = os.path.join(REPO, "tools", "variants")
-SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_nn.hip", "bb_loss.hip", "bb_conv.hip", "bb_capi.cpp", "bb_tables.cpp"]
+sys.path.insert(0, os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd"))
+from runtime.build import SOURCES  # noqa: E402  the shipped source list
 
 VARIANTS = {
     # name: extra -D flags on top of the shipped build (runtime/build.py)
@@ -57,6 +58,11 @@ VARIANTS = {
     "cfb1": ["-DBB_CONV_FWD_BOARDS=1"],
     "cfb1s32": ["-DBB_CONV_FWD_BOARDS=1", "-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
     "cm32": ["-DBB_CONV_MFMA16=0"],
+    # NHWC BatchNorm reductions: rows in flight per thread (shipped: backward 2, forward 8)
+    "bnu8": ["-DBB_BN_UNROLL_BWD=8"],
+    "bnu4": ["-DBB_BN_UNROLL_BWD=4"],  # the round-2 default before bnab
+    "bnu2": ["-DBB_BN_UNROLL_BWD=2"],
+    "bnf16": ["-DBB_BN_UNROLL_FWD=16"],
     "cw16": ["-DBB_CONV_WG16=1"],
     "cst0": ["-DBB_CONV_STORE_LDS=0"],
     "cdiag1": ["-DBB_CONV_DIAG=1"],
