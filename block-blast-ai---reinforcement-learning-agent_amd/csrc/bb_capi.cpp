@@ -570,21 +570,46 @@ extern "C" int64_t bb_bn_workspace_bytes(int32_t dtype, int32_t nhwc, int32_t N,
   return bn_workspace_bytes(dtype, nhwc, N, C, HW);
 }
 
+namespace {
+int bn_forward_impl(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW,
+                    const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps, int32_t relu,
+                    double* d_ws, float* d_save_mean, float* d_save_invstd, float* d_running_mean,
+                    float* d_running_var, float momentum, int64_t* d_num_batches_tracked, void* d_y, void* stream,
+                    const char* what) {
+  int rc = bn_check(dtype, nhwc, N, C, HW);
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_weight || !d_bias || !d_ws || !d_save_mean || !d_save_invstd || !d_y)
+    return fail(nullptr, BB_ERR_ARG, std::string(what) + ": NULL argument");
+  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
+  if (d_res && reinterpret_cast<uintptr_t>(d_res) % 16 != 0)
+    return fail(nullptr, BB_ERR_ARG, "bb_bn: d_res must be 16-byte aligned");
+  hipError_t st = launch_bn_forward(d_x, d_res, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
+                                    d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum,
+                                    d_num_batches_tracked, d_y, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, what);
+  return BB_OK;
+}
+}  // namespace
+
 extern "C" int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW,
                              const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps,
                              int32_t relu, double* d_ws, float* d_save_mean, float* d_save_invstd,
                              float* d_running_mean, float* d_running_var, float momentum,
                              int64_t* d_num_batches_tracked, void* d_y, void* stream) {
-  int rc = bn_check(dtype, nhwc, N, C, HW);
-  if (rc != BB_OK) return rc;
-  if (!d_x || !d_weight || !d_bias || !d_ws || !d_save_mean || !d_save_invstd || !d_y)
-    return fail(nullptr, BB_ERR_ARG, "bb_bn_forward: NULL argument");
-  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
-  hipError_t st = launch_bn_forward(d_x, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
-                                    d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum,
-                                    d_num_batches_tracked, d_y, (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_forward");
-  return BB_OK;
+  return bn_forward_impl(d_x, nullptr, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
+                         d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum, d_num_batches_tracked,
+                         d_y, stream, "bb_bn_forward");
+}
+
+extern "C" int bb_bn_forward_res(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N,
+                                 int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
+                                 const float* d_bias, float eps, int32_t relu, double* d_ws, float* d_save_mean,
+                                 float* d_save_invstd, float* d_running_mean, float* d_running_var, float momentum,
+                                 int64_t* d_num_batches_tracked, void* d_y, void* stream) {
+  if (!d_res) return fail(nullptr, BB_ERR_ARG, "bb_bn_forward_res: NULL residual");
+  return bn_forward_impl(d_x, d_res, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
+                         d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum, d_num_batches_tracked,
+                         d_y, stream, "bb_bn_forward_res");
 }
 
 extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N, int32_t C,

@@ -93,10 +93,10 @@ hipError_t launch_gae(const float* r, const float* v, const float* d, const floa
                       float gl, float* adv, float* ret, hipStream_t s);
 
 int64_t bn_workspace_bytes(int dtype, int nhwc, int N, int C, int HW);
-hipError_t launch_bn_forward(const void* x, int dtype, int nhwc, int N, int C, int HW, const float* pb,
-                             const float* w, const float* b, float eps, int relu, double* ws, float* save_mean,
-                             float* save_invstd, float* rmean, float* rvar, float momentum, int64_t* nbt, void* y,
-                             hipStream_t s);
+hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc, int N, int C, int HW,
+                             const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
+                             float* save_mean, float* save_invstd, float* rmean, float* rvar, float momentum,
+                             int64_t* nbt, void* y, hipStream_t s);
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
                               int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s);

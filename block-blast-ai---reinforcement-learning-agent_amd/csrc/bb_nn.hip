@@ -57,6 +57,7 @@ struct Vec<float> {
   __device__ static void store(void* p, int64_t i, const float* f) {
     reinterpret_cast<float4*>(p)[i] = make_float4(f[0], f[1], f[2], f[3]);
   }
+  __device__ static float round(float x) { return x; }
 };
 template <>
 struct Vec<__hip_bfloat16> {
@@ -75,6 +76,7 @@ struct Vec<__hip_bfloat16> {
     const uint32_t r = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
     return (u & 0x7FFFFFFFu) > 0x7F800000u ? ((u >> 16) | 0x40u) : r;  // a select, not a branch
   }
+  __device__ static float round(float x) { return __uint_as_float(rne(x) << 16); }  // the bf16 tensor value
   __device__ static void store(void* p, int64_t i, const float* f) {
     uint4 v;
     v.x = rne(f[0]) | (rne(f[1]) << 16);
@@ -294,10 +296,13 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_bwd(const double* __re
 // chunks each (one channel per chunk); NHWC rows are (n, h, w) with C / V
 // chunks of V channels each.  The NHWC grid stride is a multiple of C / V, so
 // a thread's channels are fixed and their coefficients stay in registers.
+// With res (ResidualBlock, network.py:14-30: relu(bn2(conv2(.)) + x)): the BatchNorm
+// output is rounded to T as its tensor would be, the residual added in f32 and
+// the sum stored (one rounding, as torch's add), then the ReLU.
 template <typename T, bool NHWC>
-__global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restrict__ x, void* __restrict__ y,
-                                                           int64_t total, int C, int cpr, int relu,
-                                                           const float* __restrict__ coef) {
+__global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restrict__ x, const void* __restrict__ res,
+                                                           void* __restrict__ y, int64_t total, int C, int cpr,
+                                                           int relu, const float* __restrict__ coef) {
   constexpr int V = Vec<T>::N;
   constexpr int NC = NHWC ? V : 1;
   const float4* cf = reinterpret_cast<const float4*>(coef);
@@ -310,12 +315,14 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restric
   }
   for (int64_t i = g0; i < total; i += (int64_t)gridDim.x * kBnThreads) {
     if (!NHWC) k[0] = cf[(int)((i / cpr) % C) * (kCoef / 4)];
-    float f[V];
+    float f[V], fr[V];
     Vec<T>::load(x, i, f);
+    if (res) Vec<T>::load(res, i, fr);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float4& q = k[NHWC ? j : 0];  // {pb, mu, sc, sh}
-      const float v = (f[j] + q.x - q.y) * q.z + q.w;
+      float v = (f[j] + q.x - q.y) * q.z + q.w;
+      if (res) v = Vec<T>::round(v) + fr[j];
       f[j] = relu ? fmaxf(v, 0.f) : v;
     }
     Vec<T>::store(y, i, f);
@@ -432,7 +439,7 @@ Ws split_ws(double* ws, int C) {
 }
 
 template <typename T>
-hipError_t bn_forward_t(const void* x, int nhwc, int N, int C, int HW, const float* pb, const float* w,
+hipError_t bn_forward_t(const void* x, const void* res, int nhwc, int N, int C, int HW, const float* pb, const float* w,
                         const float* b, float eps, int relu, double* ws, float* save_mean, float* save_invstd,
                         float* rmean, float* rvar, float momentum, int64_t* nbt, void* y, hipStream_t s) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
@@ -442,9 +449,11 @@ hipError_t bn_forward_t(const void* x, int nhwc, int N, int C, int HW, const flo
                      pb, w, b, save_mean, save_invstd, rmean, rvar, momentum, nbt, k.coef);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
-    hipLaunchKernelGGL((bn_apply_fwd<T, true>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, relu, k.coef);
+    hipLaunchKernelGGL((bn_apply_fwd<T, true>), ge, dim3(kBnThreads), 0, s, x, res, y, p.chunks, C, p.cpr, relu,
+                       k.coef);
   else
-    hipLaunchKernelGGL((bn_apply_fwd<T, false>), ge, dim3(kBnThreads), 0, s, x, y, p.chunks, C, p.cpr, relu, k.coef);
+    hipLaunchKernelGGL((bn_apply_fwd<T, false>), ge, dim3(kBnThreads), 0, s, x, res, y, p.chunks, C, p.cpr, relu,
+                       k.coef);
   return hipGetLastError();
 }
 
@@ -474,14 +483,14 @@ int64_t bn_workspace_bytes(int dtype, int nhwc, int N, int C, int HW) {
   return (int64_t)sizeof(double) * C * (kCoef / 2 + kQ * (int64_t)p.nb);
 }
 
-hipError_t launch_bn_forward(const void* x, int dtype, int nhwc, int N, int C, int HW, const float* pb,
-                             const float* w, const float* b, float eps, int relu, double* ws, float* save_mean,
-                             float* save_invstd, float* rmean, float* rvar, float momentum, int64_t* nbt, void* y,
-                             hipStream_t s) {
+hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc, int N, int C, int HW,
+                             const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
+                             float* save_mean, float* save_invstd, float* rmean, float* rvar, float momentum,
+                             int64_t* nbt, void* y, hipStream_t s) {
   if (dtype == 1)
-    return bn_forward_t<__hip_bfloat16>(x, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean,
+    return bn_forward_t<__hip_bfloat16>(x, res, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean,
                                         rvar, momentum, nbt, y, s);
-  return bn_forward_t<float>(x, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar, momentum,
+  return bn_forward_t<float>(x, res, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar, momentum,
                              nbt, y, s);
 }
 

@@ -58,7 +58,8 @@ class BatchNorm2d(nn.BatchNorm2d):
 
 HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs on csrc/bb_conv.hip under bf16
 NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
-FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"  # bf16 Linear weights/biases cast in one launch each way
+FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"
+RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass  # bf16 Linear weights/biases cast in one launch each way
 
 
 def conv_nobias(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
@@ -119,7 +120,19 @@ class ResidualBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         y = conv_bn(self.conv1, self.bn1, x)
-        y = conv_bn(self.conv2, self.bn2, y)
+        bn2, conv2 = self.bn2, self.conv2
+        if (RES_FUSED and isinstance(bn2, BatchNorm2d) and conv2.bias is not None and bn2.training and x.is_cuda
+                and bn2.use_fused):
+            z = conv_nobias(conv2, y)
+            from runtime.kernels import BatchNormAddReLUFunction, _bn_layout
+
+            if bn2.fusable(z) and x.dtype == z.dtype and x.shape == z.shape and _bn_layout(x) == _bn_layout(z):
+                # bn2 -> + identity -> relu in the BatchNorm apply pass
+                return BatchNormAddReLUFunction.apply(z, conv2.bias, x, bn2.weight, bn2.bias, bn2.running_mean,
+                                                      bn2.running_var, bn2.momentum, bn2.eps,
+                                                      bn2.num_batches_tracked)
+            return F.relu(bn2(z, pre_bias=conv2.bias) + x)
+        y = conv_bn(conv2, bn2, y)
         return F.relu(y + x)
 
 

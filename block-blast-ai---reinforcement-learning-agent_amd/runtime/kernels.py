@@ -199,6 +199,55 @@ class BatchNormReLUFunction(torch.autograd.Function):
         return dx, dpb, dw, db, None, None, None, None, None, None
 
 
+class BatchNormAddReLUFunction(torch.autograd.Function):
+    """relu(batch_norm(x + pre_bias) + res) with running-stat update: the tail
+    of ResidualBlock (network.py:14-30, bn2 -> + identity -> relu) in the
+    BatchNorm apply pass (bb_bn_forward_res) instead of two more elementwise
+    passes.  Backward: the ReLU mask from the saved output (torch's
+    threshold_backward, as F.relu's backward), which is also the residual's
+    gradient, then bb_bn_backward without ReLU."""
+
+    @staticmethod
+    def forward(ctx, x, pre_bias, res, weight, bias, running_mean, running_var, momentum: float, eps: float,
+                num_batches_tracked=None):
+        nhwc = _bn_layout(x)
+        fmt = torch.channels_last if nhwc else torch.contiguous_format
+        x = x.contiguous(memory_format=fmt)
+        res = res.contiguous(memory_format=fmt)
+        n, c, h, w = x.shape
+        dev = x.device
+        y = torch.empty_like(x)
+        ws = _bn_workspace(x, nhwc)
+        mean = torch.empty(c, dtype=torch.float32, device=dev)
+        invstd = torch.empty(c, dtype=torch.float32, device=dev)
+        L.check(L.load().bb_bn_forward_res(_p(x), _p(res), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias),
+                                           _p(weight), _p(bias), float(eps), 1, _p(ws), _p(mean), _p(invstd),
+                                           _p(running_mean), _p(running_var), float(momentum),
+                                           _p(num_batches_tracked), _p(y), _s(dev)),
+                "bb_bn_forward_res")
+        ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd, y)
+        ctx.nhwc = nhwc
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, pre_bias, weight, bias, mean, invstd, y = ctx.saved_tensors
+        fmt = torch.channels_last if ctx.nhwc else torch.contiguous_format
+        g = torch.ops.aten.threshold_backward(dy.to(x.dtype), y, 0).contiguous(memory_format=fmt)
+        n, c, h, w = x.shape
+        dev = x.device
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(weight)
+        db = torch.empty_like(bias)
+        dpb = torch.empty_like(pre_bias) if pre_bias is not None else None
+        ws = _bn_workspace(x, ctx.nhwc)
+        L.check(L.load().bb_bn_backward(_p(x), _p(g), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w, _p(pre_bias),
+                                        _p(weight), _p(bias), _p(mean), _p(invstd), 0, _p(ws), _p(dx), _p(dw),
+                                        _p(db), _p(dpb), _s(dev)),
+                "bb_bn_backward")
+        return dx, dpb, g, dw, db, None, None, None, None, None
+
+
 # ---------------------------------------------------------------------------
 # 3x3 / pad-1 convolutions over 8x8 boards, bf16 MFMA (csrc/bb_conv.hip)
 # ---------------------------------------------------------------------------
@@ -379,11 +428,17 @@ class LinearCastFunction(torch.autograd.Function):
         outs = [torch.empty(p.shape, dtype=torch.bfloat16, device=p.device) for p in params]
         cast_multi(0, params, outs, perms)
         ctx.perms = perms
+        ctx.set_materialize_grads(False)  # an unused output leaves its parameter's .grad None, as autocast does
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *grads):
-        gin = [g.to(torch.bfloat16).contiguous() for g in grads]
-        outs = [torch.empty(g.shape, dtype=torch.float32, device=g.device) for g in gin]
-        cast_multi(1, gin, outs, ctx.perms)
-        return (None, *outs)
+        idx = [i for i, g in enumerate(grads) if g is not None]
+        res = [None] * len(grads)
+        if idx:
+            gin = [grads[i].to(torch.bfloat16).contiguous() for i in idx]
+            outs = [torch.empty(g.shape, dtype=torch.float32, device=g.device) for g in gin]
+            cast_multi(1, gin, outs, [ctx.perms[i] for i in idx])
+            for i, o in zip(idx, outs):
+                res[i] = o
+        return (None, *res)

@@ -134,6 +134,8 @@ SIGNATURES = {
     "bb_bn_workspace_bytes": (C.c_int64, [_I32, _I32, _I32, _I32, _I32]),
     "bb_bn_forward": (C.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P, _F, _P, _P,
                                 _P]),
+    "bb_bn_forward_res": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P,
+                                    _F, _P, _P, _P]),
     "bb_bn_backward": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                  _P]),
     "bb_conv3x3_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),

@@ -283,6 +283,18 @@ int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32_t N, int32
                   int32_t relu, double* d_ws, float* d_save_mean, float* d_save_invstd,
                   float* d_running_mean, float* d_running_var, float momentum,
                   int64_t* d_num_batches_tracked, void* d_y, void* stream);
+/* bb_bn_forward with a residual input (ResidualBlock, network.py:14-30:
+ * relu(bn2(conv2(.)) + x)): y = [relu](round(BatchNorm(x + pre_bias)) + res),
+ * where round is the activation dtype's rounding (the BatchNorm output tensor
+ * of the unfused module) and the sum is rounded once, as torch's add.  d_res
+ * has x's shape, dtype and layout (16-byte aligned).  The backward is
+ * bb_bn_backward with relu = 0 over dy masked by y > 0 (the caller's
+ * threshold_backward), whose masked dy is also the residual's gradient. */
+int bb_bn_forward_res(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N,
+                      int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
+                      const float* d_bias, float eps, int32_t relu, double* d_ws, float* d_save_mean,
+                      float* d_save_invstd, float* d_running_mean, float* d_running_var, float momentum,
+                      int64_t* d_num_batches_tracked, void* d_y, void* stream);
 int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N,
                    int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                    const float* d_bias, const float* d_save_mean, const float* d_save_invstd,

@@ -1,4 +1,4 @@
-"""GPU parity of the minibatch-step tail (csrc/bb_optim.hip), through the C-ABI.
+"""GPU parity of the minibatch-step fusions (csrc/bb_optim.hip, bb_bn_forward_res), through the C-ABI.
 
 bb_adam_clip_step vs torch's own nn.utils.clip_grad_norm_ + torch.optim.Adam
 (fp32, the reference's ppo.py:400-401): parameters, moments and clipped
@@ -6,7 +6,8 @@ gradients within 2e-6 relative or 2e-7 of the largest element (the norm is summe
 fp32 by torch), step counts equal, run-to-run bit-identical.
 bb_cast_multi: bit-exact against torch's .to(bfloat16) / .float() casts,
 permuted and not.  The network's bf16 forward / backward with the multi-tensor
-casts == autocast's per-tensor casts, bit for bit.
+casts == autocast's per-tensor casts, bit for bit.  The ResidualBlock tail fused
+into the BatchNorm pass == BatchNorm -> add -> relu, bit for bit.
 """
 import pytest
 import torch
@@ -146,3 +147,68 @@ def test_network_fused_casts_equal_autocast(cuda, monkeypatch):
             assert torch.equal(gr, res[False][2][n]), n
         else:
             assert torch.allclose(gr, res[False][2][n], rtol=1e-2, atol=1e-4), n
+
+
+@pytest.mark.parametrize("dtype,nhwc", [(torch.float32, False), (torch.float32, True), (torch.bfloat16, True)])
+def test_bn_add_relu_equals_composite(cuda, dtype, nhwc):
+    """BatchNormAddReLUFunction == BatchNormReLUFunction(relu=False) -> + res ->
+    relu, forward, running statistics and every gradient, bit for bit."""
+    from runtime import kernels as K
+
+    g = torch.Generator(device=cuda).manual_seed(11)
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    n, c = 96, 128
+    x0 = (torch.randn((n, c, 8, 8), device=cuda, generator=g) * 2 + 0.5).to(dtype).contiguous(memory_format=fmt)
+    r0 = torch.randn((n, c, 8, 8), device=cuda, generator=g).to(dtype).contiguous(memory_format=fmt)
+    pb0 = torch.randn(c, device=cuda, generator=g) * 0.1
+    w0 = torch.rand(c, device=cuda, generator=g) + 0.5
+    b0 = torch.randn(c, device=cuda, generator=g) * 0.1
+    dy = torch.randn((n, c, 8, 8), device=cuda, generator=g).to(dtype).contiguous(memory_format=fmt)
+    outs = []
+    for fused in (True, False):
+        x, r, pb, w, b = (t.clone().requires_grad_(True) for t in (x0, r0, pb0, w0, b0))
+        rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+        nbt = torch.zeros((), dtype=torch.long, device=cuda)
+        if fused:
+            y = K.BatchNormAddReLUFunction.apply(x, pb, r, w, b, rm, rv, 0.1, 1e-5, nbt)
+        else:
+            y = torch.relu(K.BatchNormReLUFunction.apply(x, pb, w, b, rm, rv, 0.1, 1e-5, False, nbt) + r)
+        y.backward(dy)
+        outs.append([y.detach(), rm, rv, nbt, x.grad, r.grad, pb.grad, w.grad, b.grad])
+    for i, (a, bb) in enumerate(zip(*outs)):
+        assert torch.equal(a, bb), i
+
+
+def test_network_res_fused_equals_unfused(cuda, monkeypatch):
+    """bf16 training forward + backward of the whole CNN with the ResidualBlock
+    tail fused and not: logits, values, BatchNorm statistics and gradients."""
+    import models.network as N
+
+    torch.manual_seed(1)
+    net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    net.train()
+    x = (torch.rand((128, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(N, "RES_FUSED", fused)
+        net.load_state_dict(state0)
+        net.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            lo, va = net.raw(x)
+        (lo.float().square().mean() + va.float().sum()).backward()
+        res[fused] = (lo.detach().float(), va.detach().float(),
+                      {n: p.grad.clone() for n, p in net.named_parameters()},
+                      {k: v.clone() for k, v in net.state_dict().items()})
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
+    for k, v in res[True][3].items():
+        assert torch.equal(v, res[False][3][k]), k
+    for n, gr in res[True][2].items():
+        if n.startswith("conv_encoder.0."):  # MIOpen's first-layer weight gradient may differ in the last bits
+            assert torch.allclose(gr, res[False][2][n], rtol=1e-2, atol=1e-4), n
+        else:
+            assert torch.equal(gr, res[False][2][n]), n
