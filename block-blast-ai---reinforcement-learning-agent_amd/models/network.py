@@ -59,6 +59,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs on csrc/bb_conv.hip under bf16
 NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
 FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"
+LINEAR_RELU = os.environ.get("BB_LINEAR_RELU", "1") != "0"  # bf16 Linear -> ReLU: the ReLU in the GEMM epilogue
 RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass  # bf16 Linear weights/biases cast in one launch each way
 
 
@@ -224,11 +225,28 @@ class BlockBlastNetwork(nn.Module):
         return sh
 
     @staticmethod
-    def _run(seq: nn.Sequential, z: torch.Tensor, sh, skip_first: bool = False) -> torch.Tensor:
-        for i, m in enumerate(seq):
-            if skip_first and i == 0:
-                continue
-            z = F.linear(z, *sh[m]) if (sh is not None and isinstance(m, nn.Linear)) else m(z)
+    def _run(seq: nn.Sequential, z: torch.Tensor, sh, skip_first: bool = False, relu_first: bool = False) -> torch.Tensor:
+        """seq(z), its Linear layers on the bf16 shadows ``sh`` when given; a
+        Linear followed by a ReLU then runs as one GEMM with the ReLU in its
+        epilogue (LinearReLUFunction).  skip_first: seq[0] was applied already
+        (relu_first: with the following ReLU)."""
+        mods = list(seq)
+        i = 1 if skip_first else 0
+        if skip_first and relu_first:
+            i = 2
+        while i < len(mods):
+            m = mods[i]
+            if sh is not None and isinstance(m, nn.Linear):
+                if LINEAR_RELU and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU) and z.dim() == 2:
+                    from runtime.kernels import LinearReLUFunction
+
+                    z = LinearReLUFunction.apply(z, *sh[m])
+                    i += 2
+                    continue
+                z = F.linear(z, *sh[m])
+            else:
+                z = m(z)
+            i += 1
         return z
 
     def _trunk(self, x: torch.Tensor):
@@ -246,7 +264,14 @@ class BlockBlastNetwork(nn.Module):
             flat = h.permute(0, 2, 3, 1).reshape(n, hh * ww * c)
             sh = self._linear_shadows(h, (c, hh * ww))
             if sh is not None:  # the permuted bf16 weight comes out of the multi-tensor cast
-                return self._run(self.fc_encoder, F.linear(flat, *sh[lin0]), sh, skip_first=True), sh
+                fuse = LINEAR_RELU and len(self.fc_encoder) > 1 and isinstance(self.fc_encoder[1], nn.ReLU)
+                if fuse:
+                    from runtime.kernels import LinearReLUFunction
+
+                    z = LinearReLUFunction.apply(flat, *sh[lin0])
+                else:
+                    z = F.linear(flat, *sh[lin0])
+                return self._run(self.fc_encoder, z, sh, skip_first=True, relu_first=fuse), sh
             wp = lin0.weight.view(o, c, hh, ww).permute(0, 2, 3, 1)
             if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
                 wp = wp.to(torch.bfloat16, memory_format=torch.contiguous_format)  # autocast's cast + the permute, one pass

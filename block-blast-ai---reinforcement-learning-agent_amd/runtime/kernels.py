@@ -412,6 +412,28 @@ def cast_multi(dir_: int, srcs, dsts, perms) -> None:
             "bb_cast_multi")
 
 
+class LinearReLUFunction(torch.autograd.Function):
+    """relu(F.linear(x, w, b)) for 2-D x with the ReLU in hipBLASLt's GEMM
+    epilogue (torch._addmm_activation; one kernel instead of the GEMM and a
+    clamp pass).  Backward as autograd's: the mask from the saved output
+    (threshold_backward, F.relu's rule), then dx = g w, dw = g^T x, db = sum g."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        y = torch._addmm_activation(bias, x, weight.t())
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        g = torch.ops.aten.threshold_backward(gy, y, 0)
+        dx = g.mm(weight) if ctx.needs_input_grad[0] else None
+        dw = g.t().mm(x) if ctx.needs_input_grad[1] else None
+        db = g.sum(0) if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
 class LinearCastFunction(torch.autograd.Function):
     """autocast's f32 -> bf16 casts of the CNN's Linear weights and biases, all
     in one launch, and the bf16 -> f32 casts of their gradients in one launch

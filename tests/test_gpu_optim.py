@@ -122,6 +122,7 @@ def test_network_fused_casts_equal_autocast(cuda, monkeypatch):
     same logits, values and parameter gradients as autocast's own casts."""
     import models.network as N
 
+    monkeypatch.setattr(N, "LINEAR_RELU", False)  # the casts alone (the epilogue ReLU has its own test)
     torch.manual_seed(0)
     net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
     for mod in net.modules():
@@ -212,3 +213,26 @@ def test_network_res_fused_equals_unfused(cuda, monkeypatch):
             assert torch.allclose(gr, res[False][2][n], rtol=1e-2, atol=1e-4), n
         else:
             assert torch.equal(gr, res[False][2][n]), n
+
+
+def test_linear_relu_epilogue(cuda):
+    """LinearReLUFunction (ReLU in the GEMM epilogue) vs relu(F.linear) in bf16:
+    outputs within one bf16 rounding, gradients within bf16 accumulation noise."""
+    from runtime import kernels as K
+
+    g = torch.Generator(device=cuda).manual_seed(4)
+    x0 = torch.randn((2048, 512), device=cuda, generator=g).to(torch.bfloat16)
+    w0 = (torch.randn((256, 512), device=cuda, generator=g) * 0.05).to(torch.bfloat16)
+    b0 = (torch.randn(256, device=cuda, generator=g) * 0.1).to(torch.bfloat16)
+    gy = torch.randn((2048, 256), device=cuda, generator=g).to(torch.bfloat16)
+    outs = []
+    for fused in (True, False):
+        x, w, b = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+        y = K.LinearReLUFunction.apply(x, w, b) if fused else torch.relu(torch.nn.functional.linear(x, w, b))
+        y.backward(gy)
+        outs.append((y.detach().float(), x.grad.float(), w.grad.float(), b.grad.float()))
+    (y1, *g1), (y2, *g2) = outs
+    assert torch.allclose(y1, y2, rtol=8e-3, atol=1e-3)
+    assert ((y1 > 0) == (y2 > 0)).float().mean() > 0.999
+    for a, bb in zip(g1, g2):
+        assert float((a - bb).norm() / bb.norm()) < 1e-2
