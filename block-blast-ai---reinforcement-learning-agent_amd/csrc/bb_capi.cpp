@@ -687,6 +687,24 @@ extern "C" int bb_conv3x3_prep(const float* d_w, int32_t cin, int32_t cout, int3
   return BB_OK;
 }
 
+extern "C" int bb_conv3x3_prep_multi(int32_t num_layers, const float* const* h_w, const int32_t* h_cin,
+                                     const int32_t* h_cout, const int32_t* h_w_layout, void* const* h_wf,
+                                     void* const* h_wd, void* stream) {
+  if (num_layers <= 0 || num_layers > 16)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_prep_multi: 1 to 16 layers");
+  if (!h_w || !h_cin || !h_cout || !h_w_layout || !h_wf || !h_wd)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_prep_multi: NULL argument");
+  for (int l = 0; l < num_layers; ++l)
+    if (!al16(h_wf[l]) || !al16(h_wd[l]))
+      return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_prep_multi: outputs must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_prep_multi(num_layers, h_w, h_cin, h_cout, h_w_layout, h_wf, h_wd,
+                                            (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_prep_multi: NULL weight/output, channels not 64/128 or bad layout");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_prep_multi");
+  return BB_OK;
+}
+
 extern "C" int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
                                   void* stream) {
   int rc = conv_check(N, cin, cout, "bb_conv3x3_forward");

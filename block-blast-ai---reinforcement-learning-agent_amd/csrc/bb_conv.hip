@@ -71,6 +71,32 @@ __global__ void __launch_bounds__(kThreads) conv_prep_kernel(const float* __rest
   wd[((8 - t) * cin + ci) * cout + co] = b;
 }
 
+// All layers' weight prep in one launch (one kernel per layer otherwise): the
+// table of up to kPrepMax layers travels in the kernel arguments.
+constexpr int kPrepMax = 16;
+struct PrepTable {
+  const float* w[kPrepMax];
+  uint16_t* wf[kPrepMax];
+  uint16_t* wd[kPrepMax];
+  int cin[kPrepMax], cout[kPrepMax], wl[kPrepMax];
+  int block0[kPrepMax + 1];  // first workgroup of layer l
+  int count;
+};
+
+__global__ void __launch_bounds__(kThreads) conv_prep_multi_kernel(const PrepTable tab) {
+  int l = 0;
+  while (l + 1 < tab.count && tab.block0[l + 1] <= (int)blockIdx.x) ++l;
+  const int cout = tab.cout[l], cin = tab.cin[l], wl = tab.wl[l];
+  const int i = (blockIdx.x - tab.block0[l]) * kThreads + threadIdx.x;
+  if (i >= cout * cin * 9) return;
+  const int co = i / (9 * cin);
+  const int t = wl ? (i / cin) % 9 : i % 9;
+  const int ci = wl ? i % cin : (i / 9) % cin;
+  const uint16_t b = f2bf(tab.w[l][i]);
+  tab.wf[l][(t * cout + co) * cin + ci] = b;
+  tab.wd[l][((8 - t) * cin + ci) * cout + co] = b;
+}
+
 // LDS image of pixel rows of C bf16 channels: 16-byte chunk c of row r sits at
 // chunk c ^ key(r), so 16 lanes reading one chunk of 16 consecutive rows hit
 // 16 different bank groups (256-B rows: key = r & 15; 128-B rows, two per bank
@@ -712,6 +738,29 @@ hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* 
   const int n = cout * cin * 9;
   hipLaunchKernelGGL(conv_prep_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, w, cout, cin, wl,
                      (uint16_t*)wf, (uint16_t*)wd);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
+                                     const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s) {
+  if (count <= 0 || count > kPrepMax) return hipErrorInvalidValue;
+  PrepTable tab;
+  tab.count = count;
+  int blocks = 0;
+  for (int l = 0; l < count; ++l) {
+    if (!w[l] || !wf[l] || !wd[l] || !conv3x3_supported(cin[l], cout[l]) || (wl[l] != 0 && wl[l] != 1))
+      return hipErrorInvalidValue;
+    tab.w[l] = w[l];
+    tab.wf[l] = static_cast<uint16_t*>(wf[l]);
+    tab.wd[l] = static_cast<uint16_t*>(wd[l]);
+    tab.cin[l] = cin[l];
+    tab.cout[l] = cout[l];
+    tab.wl[l] = wl[l];
+    tab.block0[l] = blocks;
+    blocks += (cout[l] * cin[l] * 9 + kThreads - 1) / kThreads;
+  }
+  tab.block0[count] = blocks;
+  hipLaunchKernelGGL(conv_prep_multi_kernel, dim3(blocks), dim3(kThreads), 0, s, tab);
   return hipGetLastError();
 }
 

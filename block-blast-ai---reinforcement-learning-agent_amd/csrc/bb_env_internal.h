@@ -104,6 +104,8 @@ hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc
 bool conv3x3_supported(int cin, int cout);
 int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout);
 hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* wf, void* wd, hipStream_t s);
+hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
+                                     const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s);
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s);
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);

@@ -60,30 +60,36 @@ HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs
 NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
 FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"
 LINEAR_RELU = os.environ.get("BB_LINEAR_RELU", "1") != "0"  # bf16 Linear -> ReLU: the ReLU in the GEMM epilogue
+PREP_MULTI = os.environ.get("BB_PREP_MULTI", "1") != "0"  # the HIP convs' weight images in one launch
 RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass  # bf16 Linear weights/biases cast in one launch each way
 
 
-def conv_nobias(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+def _hip_conv_on(x: torch.Tensor) -> bool:
+    return HIP_CONV and x.is_cuda and torch.is_autocast_enabled("cuda") \
+        and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None) -> torch.Tensor:
     """conv(x) without its bias.  Under bf16 autocast on the GPU the 3x3
     layers with 64 or 128 channels in and out run on the HIP kernels
     (runtime.kernels.Conv3x3Function): bf16 NHWC, f32 accumulation, as
-    autocast's conv2d."""
-    if HIP_CONV and x.is_cuda and torch.is_autocast_enabled("cuda") \
-            and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+    autocast's conv2d.  ``images``: {conv: bf16 weight images} prepared for all
+    layers in one launch (BlockBlastNetwork._conv_images)."""
+    if _hip_conv_on(x):
         from runtime.kernels import Conv3x3Function, conv3x3_fusable
 
         if conv3x3_fusable(x, conv):
-            return Conv3x3Function.apply(x, conv.weight)
+            return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None)
     return conv._conv_forward(x, conv.weight, None)
 
 
-def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor) -> torch.Tensor:
+def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None) -> torch.Tensor:
     """bn(conv(x)).  When the BatchNorm runs on the HIP kernels the
     convolution's bias is added inside them (one add on load instead of a
     separate pass, and its gradient comes out of the BatchNorm backward instead
     of a reduction over dy)."""
     if isinstance(bn, BatchNorm2d) and conv.bias is not None and bn.training and x.is_cuda and bn.use_fused:
-        z = conv_nobias(conv, x)
+        z = conv_nobias(conv, x, images)
         if bn.fusable(z):
             return bn(z, pre_bias=conv.bias)
         return bn(z + conv.bias.view(1, -1, 1, 1).to(z.dtype))
@@ -94,16 +100,16 @@ class ConvStack(nn.Sequential):
     """nn.Sequential (same module indices, so the same state_dict keys) that
     runs each Conv2d -> BatchNorm2d pair through conv_bn."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, images=None) -> torch.Tensor:
         mods = list(self)
         i = 0
         while i < len(mods):
             m = mods[i]
             if isinstance(m, nn.Conv2d) and i + 1 < len(mods) and isinstance(mods[i + 1], BatchNorm2d):
-                x = conv_bn(m, mods[i + 1], x)
+                x = conv_bn(m, mods[i + 1], x, images)
                 i += 2
                 continue
-            x = m(x)
+            x = m(x, images) if isinstance(m, ResidualBlock) else m(x)
             i += 1
         return x
 
@@ -119,12 +125,12 @@ class ResidualBlock(nn.Module):
         self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
         self.bn2 = BatchNorm2d(channels)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = conv_bn(self.conv1, self.bn1, x)
+    def forward(self, x: torch.Tensor, images=None) -> torch.Tensor:
+        y = conv_bn(self.conv1, self.bn1, x, images)
         bn2, conv2 = self.bn2, self.conv2
         if (RES_FUSED and isinstance(bn2, BatchNorm2d) and conv2.bias is not None and bn2.training and x.is_cuda
                 and bn2.use_fused):
-            z = conv_nobias(conv2, y)
+            z = conv_nobias(conv2, y, images)
             from runtime.kernels import BatchNormAddReLUFunction, _bn_layout
 
             if bn2.fusable(z) and x.dtype == z.dtype and x.shape == z.shape and _bn_layout(x) == _bn_layout(z):
@@ -133,7 +139,7 @@ class ResidualBlock(nn.Module):
                                                       bn2.running_var, bn2.momentum, bn2.eps,
                                                       bn2.num_batches_tracked)
             return F.relu(bn2(z, pre_bias=conv2.bias) + x)
-        y = conv_bn(conv2, bn2, y)
+        y = conv_bn(conv2, bn2, y, images)
         return F.relu(y + x)
 
 
@@ -249,9 +255,23 @@ class BlockBlastNetwork(nn.Module):
             i += 1
         return z
 
+    def _conv_images(self, x: torch.Tensor):
+        """Under bf16 autocast on the GPU: the bf16 weight images of every HIP
+        board convolution, all layers in one launch (bb_conv3x3_prep_multi)
+        instead of one prep launch per layer.  None when not applicable."""
+        if not (PREP_MULTI and self.training and _hip_conv_on(x)):  # eval: conv_bn runs torch's convolutions
+            return None
+        from runtime.kernels import conv3x3_fusable, conv3x3_prep_multi
+
+        probe = x[:1]  # 8x8 boards: every layer sees the same geometry
+        convs = [m for m in self.conv_encoder.modules() if isinstance(m, nn.Conv2d) and conv3x3_fusable(probe, m)]
+        if not convs or len(convs) > 16:
+            return None
+        return dict(zip(convs, conv3x3_prep_multi([c.weight for c in convs])))
+
     def _trunk(self, x: torch.Tensor):
         """x: (B, 4, 8, 8) -> (fc features (B, fc_hidden[-1]), Linear shadows or None)."""
-        h = self.conv_encoder(x)
+        h = self.conv_encoder(x, self._conv_images(x))
         lin0 = self.fc_encoder[0] if len(self.fc_encoder) else None
         if (NHWC_FLATTEN and isinstance(lin0, nn.Linear) and h.is_cuda
                 and h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous()):

@@ -278,17 +278,20 @@ class Conv3x3Function(torch.autograd.Function):
     kernel over dy with the tap-reversed, transposed weight image)."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, images=None):
         _need_cuda(x, weight)
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n, cin = x.shape[0], x.shape[1]
         cout = weight.shape[0]
         dev = x.device
         lib = L.load()
-        wl = _w_layout(weight)
-        wf = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
-        wd = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
-        L.check(lib.bb_conv3x3_prep(_p(weight), cin, cout, wl, _p(wf), _p(wd), _s(dev)), "bb_conv3x3_prep")
+        if images is not None:  # from conv3x3_prep_multi (all layers in one launch)
+            wf, wd = images
+        else:
+            wl = _w_layout(weight)
+            wf = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
+            wd = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
+            L.check(lib.bb_conv3x3_prep(_p(weight), cin, cout, wl, _p(wf), _p(wd), _s(dev)), "bb_conv3x3_prep")
         y = torch.empty((n, cout, 8, 8), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
         L.check(lib.bb_conv3x3_forward(_p(x), _p(wf), n, cin, cout, _p(y), _s(dev)), "bb_conv3x3_forward")
         ctx.save_for_backward(x, wd, weight)
@@ -314,7 +317,27 @@ class Conv3x3Function(torch.autograd.Function):
             dw = torch.empty_like(weight, dtype=torch.float32)
             L.check(lib.bb_conv3x3_wgrad(_p(x), _p(dy), n, cin, cout, _p(ws), _w_layout(dw), _p(dw), _s(dev)),
                     "bb_conv3x3_wgrad")
-        return dx, dw
+        return dx, dw, None
+
+
+def conv3x3_prep_multi(weights):
+    """bb_conv3x3_prep of every weight in one launch (bb_conv3x3_prep_multi):
+    [(forward image, data-gradient image)] per weight, bf16."""
+    k = len(weights)
+    if not 0 < k <= 16:
+        raise L.BBNativeError("conv3x3_prep_multi: 1 to 16 layers")
+    _need_cuda(*weights)
+    dev = weights[0].device
+    imgs = []
+    for w in weights:
+        n = w.shape[0] * w.shape[1] * 9
+        imgs.append((torch.empty(n, dtype=torch.bfloat16, device=dev), torch.empty(n, dtype=torch.bfloat16, device=dev)))
+    i32 = C.c_int32 * k
+    L.check(L.load().bb_conv3x3_prep_multi(k, _ptrs(weights), i32(*[w.shape[1] for w in weights]),
+                                           i32(*[w.shape[0] for w in weights]), i32(*[_w_layout(w) for w in weights]),
+                                           _ptrs([a for a, _ in imgs]), _ptrs([b for _, b in imgs]), _s(dev)),
+            "bb_conv3x3_prep_multi")
+    return imgs
 
 
 # ---------------------------------------------------------------------------

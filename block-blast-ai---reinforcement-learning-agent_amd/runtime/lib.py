@@ -140,6 +140,7 @@ SIGNATURES = {
                                  _P]),
     "bb_conv3x3_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
     "bb_conv3x3_prep": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
+    "bb_conv3x3_prep_multi": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P]),
     "bb_conv3x3_forward": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_conv3x3_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _P, _P]),
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),

@@ -341,6 +341,11 @@ int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const flo
 int64_t bb_conv3x3_workspace_bytes(int32_t N, int32_t cin, int32_t cout);
 int bb_conv3x3_prep(const float* d_w, int32_t cin, int32_t cout, int32_t w_layout, void* d_wf, void* d_wd,
                     void* stream);
+/* bb_conv3x3_prep for num_layers <= 16 layers in one launch (host arrays of
+ * per-layer device pointers and sizes). */
+int bb_conv3x3_prep_multi(int32_t num_layers, const float* const* h_w, const int32_t* h_cin,
+                          const int32_t* h_cout, const int32_t* h_w_layout, void* const* h_wf,
+                          void* const* h_wd, void* stream);
 int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
                        void* stream);
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,

@@ -153,9 +153,9 @@ def test_network_routes_bf16_convs_to_hip(cuda, lib, monkeypatch):
     calls = []
     orig = K.Conv3x3Function.apply
 
-    def counting(x, w):
+    def counting(x, w, images=None):
         calls.append((x.shape[1], w.shape[0]))
-        return orig(x, w)
+        return orig(x, w, images)
 
     monkeypatch.setattr(K.Conv3x3Function, "apply", counting)
     net = BlockBlastNetwork().to(cuda).train().to(memory_format=torch.channels_last)

@@ -236,3 +236,45 @@ def test_linear_relu_epilogue(cuda):
     assert ((y1 > 0) == (y2 > 0)).float().mean() > 0.999
     for a, bb in zip(g1, g2):
         assert float((a - bb).norm() / bb.norm()) < 1e-2
+
+
+def test_network_prep_multi_equals_per_layer(cuda, monkeypatch):
+    """The HIP convolutions' bf16 weight images from one bb_conv3x3_prep_multi
+    launch == one bb_conv3x3_prep per layer: the bf16 training forward and
+    backward are bit-identical."""
+    import models.network as N
+    from runtime import kernels as K
+
+    torch.manual_seed(2)
+    net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    net.train()
+    convs = [m for m in net.conv_encoder.modules() if isinstance(m, torch.nn.Conv2d) and m.in_channels >= 64]
+    for c, (wf, wd) in zip(convs, K.conv3x3_prep_multi([c.weight for c in convs])):
+        n = c.weight.shape[0] * c.weight.shape[1] * 9
+        wf1, wd1 = (torch.empty(n, dtype=torch.bfloat16, device=cuda) for _ in range(2))
+        assert K.L.load().bb_conv3x3_prep(K._p(c.weight), c.in_channels, c.out_channels, K._w_layout(c.weight),
+                                          K._p(wf1), K._p(wd1), K._s(cuda)) == 0
+        assert torch.equal(wf.view(torch.int16), wf1.view(torch.int16))
+        assert torch.equal(wd.view(torch.int16), wd1.view(torch.int16))
+    x = (torch.rand((64, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+    res = {}
+    for multi in (True, False):
+        monkeypatch.setattr(N, "PREP_MULTI", multi)
+        net.load_state_dict(state0)
+        net.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            lo, va = net.raw(x)
+        (lo.float().square().mean() + va.float().sum()).backward()
+        res[multi] = (lo.detach().float(), va.detach().float(),
+                      {n: p.grad.clone() for n, p in net.named_parameters()})
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
+    for n, gr in res[True][2].items():
+        if n.startswith("conv_encoder.0."):  # MIOpen's first-layer weight gradient may differ in the last bits
+            assert torch.allclose(gr, res[False][2][n], rtol=1e-2, atol=1e-4), n
+        else:
+            assert torch.equal(gr, res[False][2][n]), n
