@@ -192,9 +192,11 @@ class PackedRolloutBuffer:
         K.gae(self.rewards, self.values, self.dones, last_values.float(), gamma, gae_lambda,
               adv=self.advantages, ret=self.returns)
 
-    def get_minibatches(self, batch_size: int, generator: Optional[torch.Generator] = None):
+    def get_minibatches(self, batch_size: int, generator: Optional[torch.Generator] = None, out=None):
         """Yields (x (B,4,8,8), mask f32 (B,192), actions, old log-probs,
-        normalised advantages, returns) in a random order."""
+        normalised advantages, returns) in a random order.  ``out(B)`` may
+        return 6 tensors to gather into (a captured optimizer step's inputs,
+        PPOAgent.minibatch_inputs), or None."""
         total = self.buffer_size * self.num_envs
         adv = self.advantages.reshape(total)
         mean, std = _global_moments(adv)
@@ -204,6 +206,13 @@ class PackedRolloutBuffer:
         actions, logp, ret = self.actions.reshape(total), self.log_probs.reshape(total), self.returns.reshape(total)
         for start in range(0, total, batch_size):
             b = perm[start:start + batch_size]
+            dst = out(b.numel()) if out is not None else None
+            if dst is not None:  # straight into the step's input buffers: no copies before the replay
+                K.gather_obs(board, hand, mb, b, out_x=dst[0], out_mask=dst[1])
+                for src, o in zip((actions, logp, adv, ret), dst[2:]):
+                    torch.index_select(src, 0, b, out=o)
+                yield tuple(dst)
+                continue
             x, mf = K.gather_obs(board, hand, mb, b)
             yield x, mf, actions[b], logp[b], adv[b], ret[b]
 
@@ -456,9 +465,27 @@ class PPOAgent(BaseAgent):
             ent = self._graphs[key] = self._capture_step(inputs)
         graph, static_in, static_stats = ent
         for dst, src in zip(static_in, inputs):
-            dst.copy_(src)
+            if dst.data_ptr() != src.data_ptr():  # minibatch_inputs() buffers are the inputs already
+                dst.copy_(src)
         graph.replay()
         return static_stats
+
+    def minibatch_inputs(self, batch: int):
+        """The captured optimizer step's 6 input tensors for a packed minibatch
+        of ``batch`` rows (x, masks, actions, old log-probs, advantages,
+        returns), for PackedRolloutBuffer.get_minibatches(out=...) to gather
+        into; None until that step has been captured (or without graphs)."""
+        if not (self.use_graphs and self.device.type == "cuda" and _world() == 1):
+            return None
+        shapes = ((batch, 4, 8, 8), (batch, 192), (batch,), (batch,), (batch,), (batch,))
+        ent = self._graphs.get((tuple(torch.Size(s) for s in shapes), self.autocast_dtype, self.network.training))
+        if ent is None:
+            return None
+        st = ent[1]
+        want = (torch.float32, torch.float32, torch.int64, torch.float32, torch.float32, torch.float32)
+        if any(t.dtype != d or not t.is_contiguous() for t, d in zip(st, want)):
+            return None
+        return st
 
     def _capture_step(self, inputs):
         """Capture one optimizer step.  The warm-up steps that graph capture
@@ -510,7 +537,7 @@ class PPOAgent(BaseAgent):
         n = 0
         packed = hasattr(buffer, "get_minibatches")
         for _ in range(cfg.num_epochs):
-            batches = buffer.get_minibatches(bs) if packed else buffer.get_samples(bs)
+            batches = buffer.get_minibatches(bs, out=self.minibatch_inputs) if packed else buffer.get_samples(bs)
             for batch in batches:
                 if packed:
                     x, masks, actions, old_lp, adv, ret = batch

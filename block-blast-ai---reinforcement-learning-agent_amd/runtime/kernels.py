@@ -106,14 +106,22 @@ def gae(rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor, last_v
 
 
 def gather_obs(board: torch.Tensor, hand: torch.Tensor, mask_bits: torch.Tensor, index: torch.Tensor,
-               want_x: bool = True, want_mask: bool = True):
+               want_x: bool = True, want_mask: bool = True, out_x: Optional[torch.Tensor] = None,
+               out_mask: Optional[torch.Tensor] = None):
     """Packed rollout records -> network input x (n,4,8,8) f32 and f32 mask
-    (n,192) for the rows in `index` (RolloutBuffer.get_samples, ppo.py:171-213)."""
+    (n,192) for the rows in `index` (RolloutBuffer.get_samples, ppo.py:171-213),
+    into out_x / out_mask when given (contiguous f32 of those shapes)."""
     _need_cuda(board, hand, mask_bits, index)
     n = index.numel()
     dev = board.device
-    x = torch.empty((n, 4, 8, 8), dtype=torch.float32, device=dev) if want_x else None
-    mf = torch.empty((n, 192), dtype=torch.float32, device=dev) if want_mask else None
+    for o, shp in ((out_x, (n, 4, 8, 8)), (out_mask, (n, 192))):
+        if o is not None and not (o.is_cuda and o.dtype == torch.float32 and tuple(o.shape) == shp
+                                  and o.is_contiguous()):
+            raise L.BBNativeError(f"gather_obs: output must be a contiguous f32 device tensor of shape {shp}")
+    x = (out_x if out_x is not None else torch.empty((n, 4, 8, 8), dtype=torch.float32, device=dev)) \
+        if want_x else None
+    mf = (out_mask if out_mask is not None else torch.empty((n, 192), dtype=torch.float32, device=dev)) \
+        if want_mask else None
     L.check(
         L.load().bb_gather_obs(_p(board), _p(hand), _p(mask_bits), _p(index.contiguous().long()), n, _p(x), _p(mf),
                                _s(dev)),

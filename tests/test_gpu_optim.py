@@ -278,3 +278,32 @@ def test_network_prep_multi_equals_per_layer(cuda, monkeypatch):
             assert torch.allclose(gr, res[False][2][n], rtol=1e-2, atol=1e-4), n
         else:
             assert torch.equal(gr, res[False][2][n]), n
+
+
+def test_update_direct_gather_equals_copies(cuda, monkeypatch):
+    """PPOAgent.update gathering packed minibatches straight into the captured
+    step's inputs == gathering into fresh tensors and copying them in."""
+    from agents import PPOAgent, PPOConfig
+    from training.trainer import DeviceRollout
+
+    results = []
+    for direct in (True, False):
+        torch.manual_seed(5)
+        agent = PPOAgent(PPOConfig(batch_size=256, num_epochs=2), device=cuda, sample_seed=3)
+        agent.autocast_dtype = torch.bfloat16
+        agent.train()
+        if not direct:
+            monkeypatch.setattr(agent, "minibatch_inputs", lambda b: None)
+        roll = DeviceRollout(1024, 0, 1024, 42, {}, 4, cuda)
+        roll.reset()
+        roll.collect(agent)
+        torch.manual_seed(6)
+        stats = agent.update(roll.buffer, agent.values_device(roll.x), batch_size=256)
+        results.append((stats, [p.detach().clone() for p in agent.network.parameters()]))
+        roll.close()
+    # MIOpen's first-layer weight gradient (split-K with atomics) differs in the last bits from run to
+    # run, so the two agents drift by rounding only
+    for k, v in results[0][0].items():
+        assert abs(v - results[1][0][k]) <= 1e-3 * max(1.0, abs(v)), k
+    for a, b in zip(results[0][1], results[1][1]):
+        assert torch.allclose(a, b, rtol=1e-3, atol=1e-5)

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--layout", choices=["default", "nchw", "channels_last"], default="default",
                     help="conv-stack activation layout (default: the agent's own choice)")
     ap.add_argument("--no-graph", action="store_true", help="issue the update step kernel by kernel")
+    ap.add_argument("--copy-inputs", action="store_true",
+                    help="gather minibatches into fresh tensors and copy them into the captured step (pre-r02 path)")
     ap.add_argument("--graph-rollout", action="store_true",
                     help="BASELINE config 5: the rollout's T steps captured in one HIP graph and replayed")
     args = ap.parse_args()
@@ -76,7 +78,8 @@ def main():
 
     buf = roll.buffer
     buf.compute_returns_and_advantages(last, 0.99, 0.95)
-    batches = buf.get_minibatches(args.batch)
+    # as PPOAgent.update: minibatches gathered straight into the captured step's inputs
+    batches = buf.get_minibatches(args.batch, out=None if args.copy_inputs else agent.minibatch_inputs)
     done = 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -74,6 +74,11 @@ def main():
     ret = torch.randn(B, device=dev, generator=g)
     for _ in range(args.warm):
         agent.train_minibatch(x, m, a, lp, adv, ret)
+    st = agent.minibatch_inputs(B)  # the captured step's own inputs (PPOAgent.update gathers into them)
+    if st is not None:
+        for dst, src in zip(st, (x, m, a, lp, adv, ret)):
+            dst.copy_(src)
+        x, m, a, lp, adv, ret = st
     torch.cuda.synchronize()
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
