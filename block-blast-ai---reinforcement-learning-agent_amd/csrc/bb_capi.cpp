@@ -765,3 +765,20 @@ extern "C" int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_cast_multi");
   return BB_OK;
 }
+
+extern "C" int64_t bb_relu_bias_grad_workspace_bytes(int32_t rows, int32_t cols) {
+  return relu_bgrad_workspace_bytes(rows, cols);
+}
+
+extern "C" int bb_relu_bias_grad(const void* d_gy, const void* d_y, int32_t dtype, int32_t rows, int32_t cols,
+                                 float* d_ws, void* d_g, void* d_db, void* stream) {
+  if (dtype != 1) return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: bf16 (dtype 1) only");
+  if (rows <= 0 || cols <= 0 || cols % 64 != 0)
+    return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: rows > 0 and a multiple of 64 columns");
+  if (!d_gy || !d_y || !d_g || !d_db || !d_ws) return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: NULL argument");
+  if (!al16(d_gy) || !al16(d_y) || !al16(d_g))
+    return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: tensors must be 16-byte aligned");
+  hipError_t st = launch_relu_bgrad(d_gy, d_y, rows, cols, d_g, d_db, d_ws, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_relu_bias_grad");
+  return BB_OK;
+}

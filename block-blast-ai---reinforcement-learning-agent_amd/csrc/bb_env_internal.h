@@ -124,6 +124,9 @@ int64_t adam_clip_workspace_bytes(int count, const int64_t* n);
 hipError_t launch_adam_clip(int count, float* const* p, float* const* g, float* const* m, float* const* v,
                             float* const* step, const int64_t* n, double lr, double beta1, double beta2, double eps,
                             float max_norm, double* ws, float* norm_out, hipStream_t s);
+int64_t relu_bgrad_workspace_bytes(int rows, int cols);
+hipError_t launch_relu_bgrad(const void* gy, const void* y, int rows, int cols, void* g, void* db, float* ws,
+                             hipStream_t s);
 hipError_t launch_cast_multi(int count, int dir, const void* const* src, void* const* dst, const int64_t* n,
                              const int32_t* perm_c, const int32_t* perm_hw, hipStream_t s);
 

@@ -4,6 +4,7 @@ torch's current stream; nothing here falls back to CPU."""
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -443,6 +444,9 @@ def cast_multi(dir_: int, srcs, dsts, perms) -> None:
             "bb_cast_multi")
 
 
+RELU_BGRAD = os.environ.get("BB_RELU_BGRAD", "0") == "1"  # measured equal to torch's pair (1.861 vs 1.858 ms): off
+
+
 class LinearReLUFunction(torch.autograd.Function):
     """relu(F.linear(x, w, b)) for 2-D x with the ReLU in hipBLASLt's GEMM
     epilogue (torch._addmm_activation; one kernel instead of the GEMM and a
@@ -458,10 +462,24 @@ class LinearReLUFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, weight, y = ctx.saved_tensors
-        g = torch.ops.aten.threshold_backward(gy, y, 0)
+        db = None
+        if (RELU_BGRAD and ctx.needs_input_grad[2] and y.dtype == torch.bfloat16 and y.dim() == 2
+                and y.shape[1] % 64 == 0 and y.is_contiguous()):
+            # threshold_backward and the bias-gradient sum in one pass (bb_relu_bias_grad)
+            gy = gy.to(torch.bfloat16).contiguous()
+            g = torch.empty_like(y)
+            db = torch.empty(y.shape[1], dtype=torch.bfloat16, device=y.device)
+            lib = L.load()
+            ws = torch.empty((lib.bb_relu_bias_grad_workspace_bytes(y.shape[0], y.shape[1]) + 3) // 4,
+                             dtype=torch.float32, device=y.device)
+            L.check(lib.bb_relu_bias_grad(_p(gy), _p(y), 1, y.shape[0], y.shape[1], _p(ws), _p(g), _p(db),
+                                          _s(y.device)),
+                    "bb_relu_bias_grad")
+        else:
+            g = torch.ops.aten.threshold_backward(gy, y, 0)
+            db = g.sum(0) if ctx.needs_input_grad[2] else None
         dx = g.mm(weight) if ctx.needs_input_grad[0] else None
         dw = g.t().mm(x) if ctx.needs_input_grad[1] else None
-        db = g.sum(0) if ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

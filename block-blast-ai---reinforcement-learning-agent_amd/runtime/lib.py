@@ -149,6 +149,8 @@ SIGNATURES = {
     "bb_adam_clip_workspace_bytes": (C.c_int64, [_I32, _P]),
     "bb_adam_clip_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double, _F,
                                     _P, _P, _P]),
+    "bb_relu_bias_grad_workspace_bytes": (C.c_int64, [_I32, _I32]),
+    "bb_relu_bias_grad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     "bb_cast_multi": (C.c_int, [_I32, _I32, _P, _P, _P, _P, _P, _P]),
 }
 

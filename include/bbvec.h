@@ -371,6 +371,17 @@ int bb_adam_clip_step(int32_t num_tensors, float* const* h_param, float* const* 
                       const int64_t* h_numel, double lr, double beta1, double beta2, double eps,
                       float max_norm, double* d_ws, float* d_total_norm, void* stream);
 
+/* Backward of a bf16 nn.Linear -> nn.ReLU (network.py:89-117) above the GEMMs:
+ * g = gy where y > 0 else 0 (torch threshold_backward on the ReLU output y)
+ * and the Linear bias gradient db = sum over rows of g (f32 accumulation in a
+ * fixed order, bf16 result as torch's bf16 sum).  gy, y, g: row-major
+ * [rows][cols] bf16, 16-byte aligned, cols a multiple of 64; db [cols] bf16;
+ * d_ws f32 scratch of bb_relu_bias_grad_workspace_bytes(rows, cols) bytes.
+ * dtype must be 1 (bf16).  Two launches, no atomics (deterministic). */
+int64_t bb_relu_bias_grad_workspace_bytes(int32_t rows, int32_t cols);
+int bb_relu_bias_grad(const void* d_gy, const void* d_y, int32_t dtype, int32_t rows, int32_t cols,
+                      float* d_ws, void* d_g, void* d_db, void* stream);
+
 /* bf16 autocast's parameter casts for the CNN's nn.Linear layers
  * (network.py:89-117 under torch.autocast), all tensors in one launch: dir 0
  * casts f32 -> bf16 (round to nearest even), dir 1 bf16 -> f32 (their
