@@ -782,3 +782,27 @@ extern "C" int bb_relu_bias_grad(const void* d_gy, const void* d_y, int32_t dtyp
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_relu_bias_grad");
   return BB_OK;
 }
+
+extern "C" int64_t bb_conv_in_workspace_bytes(int32_t N) { return conv_in_wgrad_workspace_bytes(N); }
+
+extern "C" int bb_conv_in_forward(const float* d_x, const float* d_w, int32_t w_layout, int32_t N, void* d_y,
+                                  void* stream) {
+  if (N <= 0 || (w_layout != 0 && w_layout != 1))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: N > 0, w_layout 0 or 1");
+  if (!d_x || !d_w || !d_y) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: NULL argument");
+  if (!al16(d_x) || !al16(d_y)) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: x, y must be 16-byte aligned");
+  hipError_t st = launch_conv_in_forward(d_x, d_w, w_layout, N, d_y, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_forward");
+  return BB_OK;
+}
+
+extern "C" int bb_conv_in_wgrad(const float* d_x, const void* d_dy, int32_t N, float* d_ws, int32_t w_layout,
+                                float* d_dw, void* stream) {
+  if (N <= 0 || (w_layout != 0 && w_layout != 1))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: N > 0, w_layout 0 or 1");
+  if (!d_x || !d_dy || !d_ws || !d_dw) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: NULL argument");
+  if (!al16(d_x) || !al16(d_dy)) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: x, dy must be 16-byte aligned");
+  hipError_t st = launch_conv_in_wgrad(d_x, d_dy, N, d_ws, w_layout, d_dw, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_wgrad");
+  return BB_OK;
+}

@@ -723,6 +723,131 @@ hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, flo
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// The input layer (the first Conv2d 4 -> 64 of the conv stack, network.py:75-117)
+// under bf16 autocast: x f32 NHWC [N][8][8][4] and the f32 weight are rounded to
+// bf16 in-kernel (autocast's casts), f32 accumulation, y bf16 NHWC
+// [N][64 px][64] without bias.  0.6 GFLOP per 2,048 boards: no MFMA tiling, one
+// thread per pixel and all 64 output channels (weights broadcast from LDS).
+// Weight gradient: thread (co, ci) of a workgroup accumulates the nine taps over
+// kInWgBoards boards -> partials [chunk][t][co][ci], summed in chunk order by
+// conv_wgrad_reduce (no atomics, deterministic).  MIOpen's version of this layer
+// cost a split-K weight-gradient kernel plus zero fills and casts.
+// ---------------------------------------------------------------------------
+constexpr int kInCout = 64, kInCin = 4;
+constexpr int kInCg = 16;        // forward: output channels per thread (4 channel groups x 64 pixels = 256 threads)
+constexpr int kInWgBoards = 8;   // weight gradient: boards per workgroup
+constexpr int kInWgThreads = 512;
+
+__device__ __forceinline__ float bf16r(float f) { return __uint_as_float(uint32_t(f2bf(f)) << 16); }
+
+// forward: kInBoards boards per workgroup (the weight staging amortised over them); wave g computes channels
+// [16g, 16g + 16) of a board's 64 pixels (weights broadcast from LDS)
+constexpr int kInBoards = 1;  // 1: 28.8 us per 2,048 boards; 4 (staging amortised, boards looped): slower
+__global__ void __launch_bounds__(kThreads) conv_in_fwd_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ w, int wl, int nb,
+                                                               uint16_t* __restrict__ y) {
+  __shared__ float4 ws[kInCout][9];           // [co][t] = 4 input channels, rounded to bf16
+  __shared__ float4 xs[kInBoards * 64 + 1];   // + one zero row for off-board taps
+  for (int i = threadIdx.x; i < kInCout * 9; i += kThreads) {
+    const int co = i / 9, t = i % 9;
+    float v[kInCin];
+#pragma unroll
+    for (int ci = 0; ci < kInCin; ++ci) v[ci] = bf16r(w[wl ? (co * 9 + t) * kInCin + ci : (co * kInCin + ci) * 9 + t]);
+    ws[co][t] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  const int b0 = blockIdx.x * kInBoards, nbb = min(kInBoards, nb - b0);
+  for (int i = threadIdx.x; i < kInBoards * 64; i += kThreads) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < nbb * 64) {
+      v = reinterpret_cast<const float4*>(x)[(size_t)b0 * 64 + i];
+      v = make_float4(bf16r(v.x), bf16r(v.y), bf16r(v.z), bf16r(v.w));
+    }
+    xs[i] = v;
+  }
+  if (threadIdx.x == 0) xs[kInBoards * 64] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const int p = threadIdx.x & 63, cg = threadIdx.x >> 6;
+  const int py = p >> 3, pc = p & 7;
+  for (int bb = 0; bb < nbb; ++bb) {
+    float4 patch[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = py + t / 3 - 1, xc = pc + t % 3 - 1;
+      patch[t] = xs[((unsigned)yy < 8u && (unsigned)xc < 8u) ? bb * 64 + yy * 8 + xc : kInBoards * 64];
+    }
+    float acc[kInCg];
+#pragma unroll
+    for (int j = 0; j < kInCg; ++j) {
+      float a = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float4 q = ws[cg * kInCg + j][t];
+        a += q.x * patch[t].x;
+        a += q.y * patch[t].y;
+        a += q.z * patch[t].z;
+        a += q.w * patch[t].w;
+      }
+      acc[j] = a;
+    }
+    uint4* yo = reinterpret_cast<uint4*>(y + ((size_t)(b0 + bb) * 64 + p) * kInCout + cg * kInCg);
+    yo[0] = make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
+    yo[1] = make_uint4(pack2(acc[8], acc[9]), pack2(acc[10], acc[11]), pack2(acc[12], acc[13]),
+                       pack2(acc[14], acc[15]));
+  }
+}
+
+// weight gradient: thread (co, pixel group) accumulates all 36 (ci, t) products of its pixels; the
+// 8 pixel groups add through LDS in a fixed order -> partials [chunk][t][co][ci]
+__global__ void __launch_bounds__(kInWgThreads) conv_in_wgrad_kernel(const float* __restrict__ x,
+                                                                     const uint16_t* __restrict__ dy, int nb,
+                                                                     float* __restrict__ part) {
+  constexpr int PG = kInWgThreads / kInCout;  // pixel groups
+  __shared__ float4 xs[kInWgBoards * 64 + 1];
+  __shared__ float red[PG][36][kInCout + 1];
+  const int co = threadIdx.x & (kInCout - 1), pg = threadIdx.x >> 6;
+  const int b0 = blockIdx.x * kInWgBoards;
+  const int nbb = min(kInWgBoards, nb - b0);
+  for (int i = threadIdx.x; i < kInWgBoards * 64; i += kInWgThreads) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < nbb * 64) {
+      v = reinterpret_cast<const float4*>(x)[(size_t)b0 * 64 + i];
+      v = make_float4(bf16r(v.x), bf16r(v.y), bf16r(v.z), bf16r(v.w));
+    }
+    xs[i] = v;
+  }
+  if (threadIdx.x == 0) xs[kInWgBoards * 64] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  float acc[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) acc[k] = 0.f;
+  for (int p = pg; p < nbb * 64; p += PG) {  // dy read straight from global (coalesced 128 B per wave)
+    const float g = __uint_as_float(uint32_t(dy[((size_t)b0 * 64 + p) * kInCout + co]) << 16);
+    const int q = p & 63, py = q >> 3, pc = q & 7;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = py + t / 3 - 1, xc = pc + t % 3 - 1;
+      const float4 v = xs[((unsigned)yy < 8u && (unsigned)xc < 8u) ? (p & ~63) + yy * 8 + xc : kInWgBoards * 64];
+      acc[0 * 9 + t] += g * v.x;
+      acc[1 * 9 + t] += g * v.y;
+      acc[2 * 9 + t] += g * v.z;
+      acc[3 * 9 + t] += g * v.w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 36; ++k) red[pg][k][co] = acc[k];
+  __syncthreads();
+  const size_t n = (size_t)9 * kInCout * kInCin;
+  for (int i = threadIdx.x; i < 36 * kInCout; i += kInWgThreads) {
+    const int k = i / kInCout, c = i % kInCout;  // k = ci * 9 + t
+    float s = 0.f;
+#pragma unroll
+    for (int g2 = 0; g2 < PG; ++g2) s += red[g2][k][c];
+    const int ci = k / 9, t = k % 9;
+    part[blockIdx.x * n + (t * kInCout + c) * kInCin + ci] = s;
+  }
+}
+
 }  // namespace
 
 bool conv3x3_supported(int cin, int cout) {
@@ -761,6 +886,29 @@ hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int
   }
   tab.block0[count] = blocks;
   hipLaunchKernelGGL(conv_prep_multi_kernel, dim3(blocks), dim3(kThreads), 0, s, tab);
+  return hipGetLastError();
+}
+
+int64_t conv_in_wgrad_workspace_bytes(int nb) {
+  if (nb <= 0) return -1;
+  return (int64_t)((nb + kInWgBoards - 1) / kInWgBoards) * 9 * kInCout * kInCin * (int64_t)sizeof(float);
+}
+
+hipError_t launch_conv_in_forward(const float* x, const float* w, int wl, int nb, void* y, hipStream_t s) {
+  if (nb <= 0 || (wl != 0 && wl != 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv_in_fwd_kernel, dim3((nb + kInBoards - 1) / kInBoards), dim3(kThreads), 0, s, x, w, wl, nb,
+                     static_cast<uint16_t*>(y));
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_in_wgrad(const float* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s) {
+  if (nb <= 0 || (wl != 0 && wl != 1)) return hipErrorInvalidValue;
+  const int nchunk = (nb + kInWgBoards - 1) / kInWgBoards;
+  hipLaunchKernelGGL(conv_in_wgrad_kernel, dim3(nchunk), dim3(kInWgThreads), 0, s, x,
+                     static_cast<const uint16_t*>(dy), nb, ws);
+  const int n = 9 * kInCout * kInCin;
+  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ws, nchunk,
+                     kInCout, kInCin, wl, dw);
   return hipGetLastError();
 }
 

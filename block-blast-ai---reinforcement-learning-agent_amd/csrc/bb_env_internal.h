@@ -106,6 +106,9 @@ int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout);
 hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* wf, void* wd, hipStream_t s);
 hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
                                      const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s);
+int64_t conv_in_wgrad_workspace_bytes(int nb);
+hipError_t launch_conv_in_forward(const float* x, const float* w, int wl, int nb, void* y, hipStream_t s);
+hipError_t launch_conv_in_wgrad(const float* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s);
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s);
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);

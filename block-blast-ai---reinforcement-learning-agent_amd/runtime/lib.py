@@ -146,6 +146,9 @@ SIGNATURES = {
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),
     "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
     "bb_ppo_loss_backward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
+    "bb_conv_in_workspace_bytes": (C.c_int64, [_I32]),
+    "bb_conv_in_forward": (C.c_int, [_P, _P, _I32, _I32, _P, _P]),
+    "bb_conv_in_wgrad": (C.c_int, [_P, _P, _I32, _P, _I32, _P, _P]),
     "bb_adam_clip_workspace_bytes": (C.c_int64, [_I32, _P]),
     "bb_adam_clip_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double, _F,
                                     _P, _P, _P]),

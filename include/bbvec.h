@@ -351,6 +351,21 @@ int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin,
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
 
+/* The CNN's input layer (the first Conv2d, 1 + 3 = 4 -> 64 channels, 3x3,
+ * padding 1, network.py:75-117) under bf16 autocast: x f32 NHWC
+ * (channels_last) [N][8][8][4] and the f32 weight [64][4][3][3] (w_layout 0)
+ * or [64][3][3][4] (w_layout 1) are rounded to bf16 in the kernel as autocast
+ * casts them; accumulation f32; y = conv(x, w) without bias, bf16 NHWC
+ * [N][8][8][64].  bb_conv_in_wgrad writes the f32 weight gradient (in
+ * w_layout) for the output gradient dy (bf16 NHWC); d_ws is scratch of
+ * bb_conv_in_workspace_bytes(N) bytes; deterministic.  x, y, dy 16-byte
+ * aligned.  (No input gradient: the network input needs none.) */
+int64_t bb_conv_in_workspace_bytes(int32_t N);
+int bb_conv_in_forward(const float* d_x, const float* d_w, int32_t w_layout, int32_t N, void* d_y,
+                       void* stream);
+int bb_conv_in_wgrad(const float* d_x, const void* d_dy, int32_t N, float* d_ws, int32_t w_layout,
+                     float* d_dw, void* stream);
+
 /* The end of the PPO minibatch step (PPOAgent.update, ppo.py:400-401):
  * nn.utils.clip_grad_norm_(params, max_norm) followed by
  * torch.optim.Adam(lr, betas, eps).step() (weight decay 0, no amsgrad), over
