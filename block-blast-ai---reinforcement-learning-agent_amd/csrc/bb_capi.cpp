@@ -717,6 +717,20 @@ extern "C" int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, i
   return BB_OK;
 }
 
+extern "C" int bb_conv3x3_forward_add(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout,
+                                      const void* d_add, void* d_y, void* stream) {
+  int rc = conv_check(N, cin, cout, "bb_conv3x3_forward_add");
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_w || !d_y || !d_add) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_add: NULL argument");
+  if (!al16(d_x) || !al16(d_w) || !al16(d_y) || !al16(d_add))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_add: tensors must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream, d_add);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_add: not available in this (variant) build");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward_add");
+  return BB_OK;
+}
+
 extern "C" int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                                 int32_t w_layout, float* d_dw, void* stream) {
   int rc = conv_check(N, cin, cout, "bb_conv3x3_wgrad");

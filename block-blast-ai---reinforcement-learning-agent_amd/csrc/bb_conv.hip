@@ -182,10 +182,19 @@ __device__ __forceinline__ int wkey(int co) {
   return SCI == 32 ? (co >> 2) & 3 : (co >> 1) & 7;
 }
 
+__device__ __forceinline__ uint32_t add2_bf16(uint32_t a, uint32_t b) {  // two bf16 sums, rounded once (torch's add)
+  return pack2(__uint_as_float(a << 16) + __uint_as_float(b << 16),
+               __uint_as_float(a & 0xFFFF0000u) + __uint_as_float(b & 0xFFFF0000u));
+}
+
+// radd (NULL = none, shipped LDS-staged store path only): y = bf16(conv) + radd, rounded again -- the
+// data gradient of a ResidualBlock's first convolution plus the identity path's gradient, as autograd's
+// separate add kernel computed it
 template <int CIN, int COUT>
 __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w,
-                                                               uint16_t* __restrict__ y, int nb) {
+                                                               uint16_t* __restrict__ y, int nb,
+                                                               const uint16_t* __restrict__ radd) {
   constexpr int RB = CIN * 2;                 // bytes per pixel row
   constexpr int NCH = CIN / 8;                // 16-byte chunks per pixel row
   constexpr int FB = fwd_boards<COUT>();
@@ -329,8 +338,13 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
     const int px = e / OCH, c = e % OCH;
     if (b0 + (px >> 6) >= nb) continue;
     if (BB_CONV_DIAG == 1 && acc[0][0][0] != 1.2345e-30f) continue;
-    *reinterpret_cast<uint4*>(y + (size_t(b0) * 64 + px) * COUT + c * 8) =
-        *reinterpret_cast<const uint4*>(os + px * (COUT * 2) + ((c ^ (px & 15 & (OCH - 1))) << 4));
+    const size_t o = (size_t(b0) * 64 + px) * COUT + c * 8;
+    uint4 v = *reinterpret_cast<const uint4*>(os + px * (COUT * 2) + ((c ^ (px & 15 & (OCH - 1))) << 4));
+    if (radd) {
+      const uint4 a = *reinterpret_cast<const uint4*>(radd + o);
+      v = make_uint4(add2_bf16(v.x, a.x), add2_bf16(v.y, a.y), add2_bf16(v.z, a.z), add2_bf16(v.w, a.w));
+    }
+    *reinterpret_cast<uint4*>(y + o) = v;
   }
 #else
 #pragma unroll
@@ -701,9 +715,10 @@ int wgrad_bpc(int nb, int nchunk) {
 }
 
 template <int CIN, int COUT>
-hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s) {
+hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr) {
+  if (radd && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS)) return hipErrorInvalidValue;  // variant builds: no fused add
   hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>()), dim3(kFwdThreads), 0, s,
-                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb);
+                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd);
   return hipGetLastError();
 }
 
@@ -912,11 +927,12 @@ hipError_t launch_conv_in_wgrad(const float* x, const void* dy, int nb, float* w
   return hipGetLastError();
 }
 
-hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s) {
-  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s);
-  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s);
-  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s);
-  return fwd_t<128, 128>(x, w, nb, y, s);
+hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
+                                  const void* radd) {
+  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s, radd);
+  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd);
+  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd);
+  return fwd_t<128, 128>(x, w, nb, y, s, radd);
 }
 
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,

@@ -61,10 +61,12 @@ HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs
 # step against MIOpen's (its forward is LDS-latency-bound, 28.8 us vs 11.5 + a 5 us cast): opt-in
 HIP_CONV_IN = os.environ.get("BB_HIP_CONV_IN", "0") == "1"
 NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
-FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"
+FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"  # bf16 Linear weights/biases cast in one launch each way
 LINEAR_RELU = os.environ.get("BB_LINEAR_RELU", "1") != "0"  # bf16 Linear -> ReLU: the ReLU in the GEMM epilogue
 PREP_MULTI = os.environ.get("BB_PREP_MULTI", "1") != "0"  # the HIP convs' weight images in one launch
-RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass  # bf16 Linear weights/biases cast in one launch each way
+RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass
+# ... and the identity path's input gradient added in conv1's data-gradient store pass (no add kernel)
+RES_GRAD_FUSED = os.environ.get("BB_RES_GRAD_FUSED", "1") != "0"
 
 
 def _hip_conv_on(x: torch.Tensor) -> bool:
@@ -72,7 +74,7 @@ def _hip_conv_on(x: torch.Tensor) -> bool:
         and torch.get_autocast_dtype("cuda") == torch.bfloat16
 
 
-def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None) -> torch.Tensor:
+def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> torch.Tensor:
     """conv(x) without its bias.  Under bf16 autocast on the GPU the 3x3
     layers with 64 or 128 channels in and out run on the HIP kernels
     (runtime.kernels.Conv3x3Function): bf16 NHWC, f32 accumulation, as
@@ -82,19 +84,19 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None) -> torch.Tensor:
         from runtime.kernels import Conv3x3Function, ConvInFunction, conv3x3_fusable, conv_in_fusable
 
         if conv3x3_fusable(x, conv):
-            return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None)
+            return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox)
         if HIP_CONV_IN and conv_in_fusable(x, conv):  # the 4 -> 64 input layer
             return ConvInFunction.apply(x, conv.weight)
     return conv._conv_forward(x, conv.weight, None)
 
 
-def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None) -> torch.Tensor:
+def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None, mailbox=None) -> torch.Tensor:
     """bn(conv(x)).  When the BatchNorm runs on the HIP kernels the
     convolution's bias is added inside them (one add on load instead of a
     separate pass, and its gradient comes out of the BatchNorm backward instead
     of a reduction over dy)."""
     if isinstance(bn, BatchNorm2d) and conv.bias is not None and bn.training and x.is_cuda and bn.use_fused:
-        z = conv_nobias(conv, x, images)
+        z = conv_nobias(conv, x, images, mailbox)
         if bn.fusable(z):
             return bn(z, pre_bias=conv.bias)
         return bn(z + conv.bias.view(1, -1, 1, 1).to(z.dtype))
@@ -131,10 +133,18 @@ class ResidualBlock(nn.Module):
         self.bn2 = BatchNorm2d(channels)
 
     def forward(self, x: torch.Tensor, images=None) -> torch.Tensor:
-        y = conv_bn(self.conv1, self.bn1, x, images)
         bn2, conv2 = self.bn2, self.conv2
-        if (RES_FUSED and isinstance(bn2, BatchNorm2d) and conv2.bias is not None and bn2.training and x.is_cuda
-                and bn2.use_fused):
+        fused = (RES_FUSED and isinstance(bn2, BatchNorm2d) and conv2.bias is not None and bn2.training and x.is_cuda
+                 and bn2.use_fused)
+        mailbox = None
+        if fused and RES_GRAD_FUSED and _hip_conv_on(x) and isinstance(self.bn1, BatchNorm2d) \
+                and self.conv1.bias is not None and self.bn1.training and self.bn1.use_fused:
+            from runtime.kernels import GradMailbox, conv3x3_fusable
+
+            if conv3x3_fusable(x, self.conv1):  # conv1's data gradient adds the identity path's gradient
+                mailbox = GradMailbox()
+        y = conv_bn(self.conv1, self.bn1, x, images, mailbox)
+        if fused:
             z = conv_nobias(conv2, y, images)
             from runtime.kernels import BatchNormAddReLUFunction, _bn_layout
 
@@ -142,7 +152,8 @@ class ResidualBlock(nn.Module):
                 # bn2 -> + identity -> relu in the BatchNorm apply pass
                 return BatchNormAddReLUFunction.apply(z, conv2.bias, x, bn2.weight, bn2.bias, bn2.running_mean,
                                                       bn2.running_var, bn2.momentum, bn2.eps,
-                                                      bn2.num_batches_tracked)
+                                                      bn2.num_batches_tracked, mailbox)
+            # (an unused mailbox stays empty: conv1's data gradient is then the plain one, and autograd adds)
             return F.relu(bn2(z, pre_bias=conv2.bias) + x)
         y = conv_bn(conv2, bn2, y, images)
         return F.relu(y + x)

@@ -218,7 +218,8 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, pre_bias, res, weight, bias, running_mean, running_var, momentum: float, eps: float,
-                num_batches_tracked=None):
+                num_batches_tracked=None, grad_mailbox=None):
+        ctx.mailbox = grad_mailbox
         nhwc = _bn_layout(x)
         fmt = torch.channels_last if nhwc else torch.contiguous_format
         x = x.contiguous(memory_format=fmt)
@@ -254,7 +255,11 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
                                         _p(weight), _p(bias), _p(mean), _p(invstd), 0, _p(ws), _p(dx), _p(dw),
                                         _p(db), _p(dpb), _s(dev)),
                 "bb_bn_backward")
-        return dx, dpb, g, dw, db, None, None, None, None, None
+        gres = g
+        if ctx.mailbox is not None and ctx.needs_input_grad[2]:
+            ctx.mailbox.put(g)  # the block's first convolution adds it to its data gradient
+            gres = None
+        return dx, dpb, gres, dw, db, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -287,8 +292,9 @@ class Conv3x3Function(torch.autograd.Function):
     kernel over dy with the tap-reversed, transposed weight image)."""
 
     @staticmethod
-    def forward(ctx, x, weight, images=None):
+    def forward(ctx, x, weight, images=None, grad_mailbox=None):
         _need_cuda(x, weight)
+        ctx.mailbox = grad_mailbox
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n, cin = x.shape[0], x.shape[1]
         cout = weight.shape[0]
@@ -317,7 +323,14 @@ class Conv3x3Function(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            L.check(lib.bb_conv3x3_forward(_p(dy), _p(wd), n, cout, cin, _p(dx), _s(dev)), "bb_conv3x3_forward")
+            extra = ctx.mailbox.take() if ctx.mailbox is not None else None
+            if extra is not None:  # + the identity path's gradient of x, in the store pass
+                extra = extra.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                L.check(lib.bb_conv3x3_forward_add(_p(dy), _p(wd), n, cout, cin, _p(extra), _p(dx), _s(dev)),
+                        "bb_conv3x3_forward_add")
+            else:
+                L.check(lib.bb_conv3x3_forward(_p(dy), _p(wd), n, cout, cin, _p(dx), _s(dev)),
+                        "bb_conv3x3_forward")
         if ctx.needs_input_grad[1]:
             nbytes = lib.bb_conv3x3_workspace_bytes(n, cin, cout)
             if nbytes < 0:
@@ -326,7 +339,25 @@ class Conv3x3Function(torch.autograd.Function):
             dw = torch.empty_like(weight, dtype=torch.float32)
             L.check(lib.bb_conv3x3_wgrad(_p(x), _p(dy), n, cin, cout, _p(ws), _w_layout(dw), _p(dw), _s(dev)),
                     "bb_conv3x3_wgrad")
-        return dx, dw, None
+        return dx, dw, None, None
+
+
+class GradMailbox:
+    """Hands the identity path's gradient of a ResidualBlock input from
+    BatchNormAddReLUFunction.backward to the block's first Conv3x3Function
+    backward (which autograd runs later: it is upstream), so that the sum of the
+    two input gradients is formed in the data-gradient convolution's store pass
+    instead of a separate add kernel."""
+
+    def __init__(self):
+        self.g = None
+
+    def put(self, g):
+        self.g = g
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
 
 
 def conv_in_fusable(x: torch.Tensor, conv) -> bool:

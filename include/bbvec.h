@@ -348,6 +348,12 @@ int bb_conv3x3_prep_multi(int32_t num_layers, const float* const* h_w, const int
                           void* const* h_wd, void* stream);
 int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
                        void* stream);
+/* bb_conv3x3_forward plus a bf16 NHWC tensor d_add of y's shape, added to the
+ * bf16-rounded convolution and rounded again (torch's bf16 add): the data
+ * gradient of a ResidualBlock's first convolution with the identity path's
+ * gradient folded in (network.py:14-30). */
+int bb_conv3x3_forward_add(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout,
+                           const void* d_add, void* d_y, void* stream);
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
 

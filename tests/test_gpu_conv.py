@@ -153,9 +153,9 @@ def test_network_routes_bf16_convs_to_hip(cuda, lib, monkeypatch):
     calls = []
     orig = K.Conv3x3Function.apply
 
-    def counting(x, w, images=None):
+    def counting(x, w, *rest):
         calls.append((x.shape[1], w.shape[0]))
-        return orig(x, w, images)
+        return orig(x, w, *rest)
 
     monkeypatch.setattr(K.Conv3x3Function, "apply", counting)
     net = BlockBlastNetwork().to(cuda).train().to(memory_format=torch.channels_last)

@@ -330,3 +330,50 @@ def test_relu_bias_grad(cuda, rows, cols):
     assert torch.allclose(db.float(), want.float().sum(0), rtol=8e-3, atol=1e-2)
     assert torch.allclose(db.float(), want.sum(0).float(), rtol=1.6e-2, atol=2e-2)
     assert lib.bb_relu_bias_grad(K._p(gy), K._p(y), 1, rows, 48, K._p(ws), K._p(g), K._p(db), K._s(cuda)) != 0
+
+
+def test_network_res_grad_fused_equals_unfused(cuda, monkeypatch):
+    """The identity path's input gradient added in conv1's data-gradient store
+    pass (bb_conv3x3_forward_add) == autograd's separate add, bit for bit, for
+    the whole bf16 CNN (its other convolutions on the HIP kernels too)."""
+    import models.network as N
+
+    torch.manual_seed(8)
+    net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    net.train()
+    x = (torch.rand((256, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(N, "RES_GRAD_FUSED", fused)
+        net.load_state_dict(state0)
+        net.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            lo, va = net.raw(x)
+        (lo.float().square().mean() + va.float().sum()).backward()
+        res[fused] = {n: p.grad.clone() for n, p in net.named_parameters()}
+    for n, gr in res[True].items():
+        if n.startswith("conv_encoder.0."):  # MIOpen's first-layer weight gradient may differ in the last bits
+            assert torch.allclose(gr, res[False][n], rtol=1e-2, atol=1e-4), n
+        else:
+            assert torch.equal(gr, res[False][n]), n
+
+
+def test_conv3x3_forward_add(cuda):
+    """bb_conv3x3_forward_add == bf16(conv) + add, rounded once more."""
+    from runtime import kernels as K
+
+    g = torch.Generator(device=cuda).manual_seed(12)
+    n = 33
+    x = torch.randn((n, 128, 8, 8), device=cuda, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = torch.randn((128, 128, 3, 3), device=cuda, generator=g) * 0.04
+    a = torch.randn((n, 128, 8, 8), device=cuda, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    y0 = K.Conv3x3Function.apply(x, w)
+    wf, wd = K.conv3x3_prep_multi([w])[0]
+    y1 = torch.empty_like(y0)
+    lib = K.L.load()
+    assert lib.bb_conv3x3_forward_add(K._p(x), K._p(wf), n, 128, 128, K._p(a), K._p(y1), K._s(cuda)) == 0
+    assert torch.equal(y1.view(torch.int16), (y0 + a).view(torch.int16))
