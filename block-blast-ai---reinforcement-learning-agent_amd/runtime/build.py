@@ -20,6 +20,9 @@ HIPCC_FLAGS = [
     "-fPIC",
     "-shared",
     "-Wno-unused-result",
+    # LLVM's max-ILP machine scheduler: +0.8% on the rollout kernel (8.85e9 vs 8.78e9 env-steps/s, 3 interleaved
+    # repeats, profiles/r02/ab/schedab_*), the PPO update step unchanged; max-memory-clause was -1.8%
+    "-mllvm", "-amdgpu-sched-strategy=max-ilp",
 ]
 
 
@@ -38,7 +41,8 @@ def _stale(out: str, inputs) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = True) -> str:
-    inputs = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(REPO_DIR, "include", "bbvec.h")]
+    inputs = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(REPO_DIR, "include", "bbvec.h"),
+                                                                  os.path.abspath(__file__)]  # flags live here
     if not force and not _stale(LIB_PATH, inputs):
         return LIB_PATH
     tmp = LIB_PATH + ".tmp"

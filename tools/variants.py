@@ -16,7 +16,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd", "csrc")
 OUT = os.path.join(REPO, "tools", "variants")
 sys.path.insert(0, os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd"))
-from runtime.build import SOURCES  # noqa: E402  the shipped source list
+from runtime.build import HIPCC_FLAGS, SOURCES  # noqa: E402  the shipped source list and flags
 
 VARIANTS = {
     # name: extra -D flags on top of the shipped build (runtime/build.py)
@@ -58,6 +58,11 @@ VARIANTS = {
     "cfb1": ["-DBB_CONV_FWD_BOARDS=1"],
     "cfb1s32": ["-DBB_CONV_FWD_BOARDS=1", "-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
     "cm32": ["-DBB_CONV_MFMA16=0"],
+    # LLVM AMDGPU scheduler strategies (whole library; the rollout kernel is the one that cares); shipped:
+    # max-ilp (runtime/build.py), so "silp" == "main" and "sdef" is the LLVM default measured against it
+    "sdef": ["-mllvm", "-amdgpu-sched-strategy=default"],
+    "silp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "smem": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
     # NHWC BatchNorm reductions: rows in flight per thread (shipped: backward 2, forward 8)
     "bnu8": ["-DBB_BN_UNROLL_BWD=8"],
     "bnu4": ["-DBB_BN_UNROLL_BWD=4"],  # the round-2 default before bnab
@@ -83,8 +88,11 @@ def build(name: str) -> str:
     flags = VARIANTS[name]
     os.makedirs(OUT, exist_ok=True)
     out = os.path.join(OUT, f"libbbvec_{name}.so")
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-           "-shared", "-Wno-unused-result", *flags, f"-I{os.path.join(REPO, 'include')}",
+    base = [f for f in HIPCC_FLAGS if not f.startswith("--offload-arch")]  # the shipped flags (runtime/build.py)
+    if any(f.startswith("-amdgpu-sched-strategy") for f in flags):  # a scheduler variant replaces the shipped one
+        i = base.index("-mllvm")
+        del base[i:i + 2]
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *base, *flags, f"-I{os.path.join(REPO, 'include')}",
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
     subprocess.run(cmd, check=True)
     return out
