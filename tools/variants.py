@@ -63,6 +63,9 @@ VARIANTS = {
     "sdef": ["-mllvm", "-amdgpu-sched-strategy=default"],
     "silp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "smem": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+    # on top of the shipped max-ilp: GCN register-pressure trackers in the scheduler; -O2
+    "strk": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+    "o2": ["-O2"],
     # NHWC BatchNorm reductions: rows in flight per thread (shipped: backward 2, forward 8)
     "bnu8": ["-DBB_BN_UNROLL_BWD=8"],
     "bnu4": ["-DBB_BN_UNROLL_BWD=4"],  # the round-2 default before bnab
