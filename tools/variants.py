@@ -66,6 +66,8 @@ VARIANTS = {
     # on top of the shipped max-ilp: GCN register-pressure trackers in the scheduler; -O2
     "strk": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
     "o2": ["-O2"],
+    # "unr600" (-mllvm -unroll-threshold=600) was measured here and is now shipped (runtime/build.py)
+    "inl": ["-mllvm", "-inline-threshold=1000"],
     # NHWC BatchNorm reductions: rows in flight per thread (shipped: backward 2, forward 8)
     "bnu8": ["-DBB_BN_UNROLL_BWD=8"],
     "bnu4": ["-DBB_BN_UNROLL_BWD=4"],  # the round-2 default before bnab
