@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
-from typing import Any, Dict, Iterator, Optional, Tuple
+from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -109,6 +109,9 @@ class RolloutBuffer:
         self.returns = z(T, N)
         self.ptr = 0
         self.full = False
+        # minibatch order per epoch: None = numpy's global permutation, as the reference (ppo.py:199);
+        # or a callable total -> index array (tests inject the same order on both sides)
+        self.permutation: Optional[Callable[[int], Any]] = None
 
     def add(self, board, pieces, action_mask, action, log_prob, reward, done, value) -> None:
         d, t = self.device, self.ptr
@@ -135,6 +138,12 @@ class RolloutBuffer:
         self.advantages = adv.to(self.device)
         self.returns = ret.to(self.device)
 
+    def normalized_advantages(self) -> torch.Tensor:
+        """ppo.py:196 over the flattened advantages (moments over every rank)."""
+        adv = self.advantages.reshape(-1)
+        mean, std = _global_moments(adv)
+        return (adv - mean) / (std + 1e-8)
+
     def get_samples(self, batch_size: int) -> Iterator[Tuple[torch.Tensor, ...]]:
         """ppo.py:171-213: flatten, normalise advantages (ppo.py:196), random
         minibatches from numpy's global permutation (ppo.py:199)."""
@@ -144,11 +153,11 @@ class RolloutBuffer:
         masks = self.action_masks.reshape(total, -1)
         actions = self.actions.reshape(total)
         log_probs = self.log_probs.reshape(total)
-        adv = self.advantages.reshape(total)
         returns = self.returns.reshape(total)
-        mean, std = _global_moments(adv)
-        adv = (adv - mean) / (std + 1e-8)
-        idx = torch.from_numpy(np.random.permutation(total)).to(self.device)
+        adv = self.normalized_advantages()
+        perm = np.random.permutation(total) if self.permutation is None else self.permutation(total)
+        idx = torch.as_tensor(np.asarray(perm) if not torch.is_tensor(perm) else perm,
+                              dtype=torch.int64).to(self.device)
         for start in range(0, total, batch_size):
             b = idx[start:start + batch_size]
             yield (boards[b], pieces[b], masks[b], actions[b], log_probs[b], adv[b], returns[b])
@@ -179,10 +188,27 @@ class PackedRolloutBuffer:
         self.returns = torch.zeros((T, N), dtype=torch.float32, device=d)
         self.ptr = 0
         self.full = False
+        # minibatch order per epoch: None = torch.randperm on the device (no host round trip);
+        # "numpy" = np.random.permutation like the reference (ppo.py:199); or a callable total -> indices
+        self.permutation: Optional[Any] = None
 
     def reset(self) -> None:
         self.ptr = 0
         self.full = False
+
+    def normalized_advantages(self) -> torch.Tensor:
+        """ppo.py:196 over the flattened advantages (moments over every rank)."""
+        adv = self.advantages.reshape(-1)
+        mean, std = _global_moments(adv)
+        return (adv - mean) / (std + 1e-8)
+
+    def _permutation(self, total: int, generator: Optional[torch.Generator]) -> torch.Tensor:
+        if self.permutation is None:
+            return torch.randperm(total, device=self.device, generator=generator)
+        perm = np.random.permutation(total) if self.permutation == "numpy" else self.permutation(total)
+        if not torch.is_tensor(perm):
+            perm = torch.from_numpy(np.ascontiguousarray(perm, dtype=np.int64))
+        return perm.to(self.device, torch.int64)
 
     def advance(self) -> None:
         self.ptr += 1
@@ -198,10 +224,8 @@ class PackedRolloutBuffer:
         return 6 tensors to gather into (a captured optimizer step's inputs,
         PPOAgent.minibatch_inputs), or None."""
         total = self.buffer_size * self.num_envs
-        adv = self.advantages.reshape(total)
-        mean, std = _global_moments(adv)
-        adv = (adv - mean) / (std + 1e-8)
-        perm = torch.randperm(total, device=self.device, generator=generator)
+        adv = self.normalized_advantages()
+        perm = self._permutation(total, generator)
         board, hand, mb = self.board.reshape(total), self.hand.reshape(total), self.mask_bits.reshape(total, 3)
         actions, logp, ret = self.actions.reshape(total), self.log_probs.reshape(total), self.returns.reshape(total)
         for start in range(0, total, batch_size):
@@ -275,12 +299,33 @@ class PPOAgent(BaseAgent):
         self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if sample_seed is None else int(sample_seed)
         self.sample_step = 0
         self._flat_grad = None
-        self.autocast_dtype: Optional[torch.dtype] = None  # e.g. torch.bfloat16 for the CNN
-        # one optimizer step per minibatch replayed from a HIP graph (CUDA device, one process)
+        # bumped whenever parameter storage, layout or precision changes: captured graphs of the
+        # optimizer step (here) and of the rollout (training.trainer.DeviceRollout) are then stale
+        self.graph_epoch = 0
+        self._autocast_dtype: Optional[torch.dtype] = None  # e.g. torch.bfloat16 for the CNN
+        # one optimizer step per minibatch replayed from HIP graphs (CUDA device): one graph on one
+        # rank; with data parallelism forward + backward, then the RCCL all-reduce, then clip + Adam
         self.use_graphs = self.device.type == "cuda"
         self._graphs = {}
         self.fused_loss = True  # the minibatch loss on bb_ppo_loss_* (GPU tensors only)
-        self._adam_ws = None  # bb_adam_clip_step scratch, keyed by the parameter sizes
+        # bb_adam_clip_step scratch per parameter-size set; never dropped, since captured optimizer
+        # steps hold the workspace's address
+        self._adam_ws: Dict[Tuple[int, ...], torch.Tensor] = {}
+        # update(): keep every minibatch's 6 statistics (device tensors) in minibatch_stats (parity tests)
+        self.record_minibatch_stats = False
+        self.minibatch_stats: List[torch.Tensor] = []
+        # update(): called as f(index, stats) after every optimizer step (logging, parity tests)
+        self.minibatch_callback: Optional[Callable[[int, torch.Tensor], None]] = None
+
+    @property
+    def autocast_dtype(self) -> Optional[torch.dtype]:
+        return self._autocast_dtype
+
+    @autocast_dtype.setter
+    def autocast_dtype(self, dt: Optional[torch.dtype]) -> None:
+        if dt != self._autocast_dtype:
+            self.graph_epoch += 1
+        self._autocast_dtype = dt
 
     # ------------------------------------------------------------ helpers
     def set_channels_last(self, on: bool = True) -> None:
@@ -290,6 +335,7 @@ class PPOAgent(BaseAgent):
         self.channels_last = bool(on)
         self.network.to(memory_format=torch.channels_last if on else torch.contiguous_format)
         self._graphs = {}
+        self.graph_epoch += 1
         self._flat_grad = None  # gradient views must follow the parameters' strides
 
     def _raw(self, x: torch.Tensor):
@@ -403,9 +449,7 @@ class PPOAgent(BaseAgent):
             for p in self.network.parameters():
                 p.grad = None
             loss.backward()
-        if not self._fused_clip_adam():
-            nn.utils.clip_grad_norm_(self.network.parameters(), self.config.max_grad_norm)
-            self.optimizer.step()
+        self._clip_and_step()
 
     def _fused_clip_adam(self) -> bool:
         """clip_grad_norm_(max_grad_norm) + Adam.step() (ppo.py:400-401) on
@@ -440,21 +484,31 @@ class PPOAgent(BaseAgent):
                     and st["exp_avg"].stride() == p.stride() and st["exp_avg_sq"].stride() == p.stride()):
                 return False
         key = tuple(p.numel() for p in params)
-        if self._adam_ws is None or self._adam_ws[0] != key:
-            self._adam_ws = (key, K.adam_clip_workspace(list(key), self.device))
+        ws = self._adam_ws.get(key)
+        if ws is None:
+            ws = self._adam_ws[key] = K.adam_clip_workspace(list(key), self.device)
         b1, b2 = grp["betas"]
         K.adam_clip_step(params, [p.grad for p in params], [opt.state[p]["exp_avg"] for p in params],
                          [opt.state[p]["exp_avg_sq"] for p in params], [opt.state[p]["step"] for p in params],
-                         grp["lr"], b1, b2, grp["eps"], self.config.max_grad_norm, self._adam_ws[1])
+                         grp["lr"], b1, b2, grp["eps"], self.config.max_grad_norm, ws)
         return True
+
+    def _clip_and_step(self) -> None:
+        """clip_grad_norm_(max_grad_norm) + Adam.step() (ppo.py:397-401)."""
+        if not self._fused_clip_adam():
+            nn.utils.clip_grad_norm_(self.network.parameters(), self.config.max_grad_norm)
+            self.optimizer.step()
 
     def train_minibatch(self, x, masks, actions, old_log_probs, advantages, returns) -> torch.Tensor:
         """One PPO optimizer step on a minibatch (ppo.py:362-401): loss, backward,
         gradient all-reduce, clip, Adam.  Returns the 6 loss statistics on the
         device.  On a single CUDA device the step is captured once per minibatch
         shape into a HIP graph and replayed: a step is ~440 kernels, and issued
-        one by one from Python they left the GPU idle a third of the time."""
-        if not (self.use_graphs and x.is_cuda and _world() == 1):
+        one by one from Python they left the GPU idle a third of the time.
+        Data parallel: two graphs around the eager RCCL all-reduce of the flat
+        gradient buffer -- (zero fill, forward, loss, backward into the buffer)
+        and (average, clip, Adam) -- so the ranks keep graph replay."""
+        if not (self.use_graphs and x.is_cuda):
             loss, stats = self._minibatch_loss(x, masks, actions, old_log_probs, advantages, returns)
             self._optimizer_step(loss)
             return stats
@@ -463,11 +517,14 @@ class PPOAgent(BaseAgent):
         ent = self._graphs.get(key)
         if ent is None:
             ent = self._graphs[key] = self._capture_step(inputs)
-        graph, static_in, static_stats = ent
+        graphs, static_in, static_stats = ent
         for dst, src in zip(static_in, inputs):
             if dst.data_ptr() != src.data_ptr():  # minibatch_inputs() buffers are the inputs already
                 dst.copy_(src)
-        graph.replay()
+        graphs[0].replay()
+        if len(graphs) > 1:  # one all-reduce of the flat fp32 gradient buffer (RCCL over xGMI), then the step
+            dist.all_reduce(self._flat_grad)
+            graphs[1].replay()
         return static_stats
 
     def minibatch_inputs(self, batch: int):
@@ -475,7 +532,7 @@ class PPOAgent(BaseAgent):
         of ``batch`` rows (x, masks, actions, old log-probs, advantages,
         returns), for PackedRolloutBuffer.get_minibatches(out=...) to gather
         into; None until that step has been captured (or without graphs)."""
-        if not (self.use_graphs and self.device.type == "cuda" and _world() == 1):
+        if not (self.use_graphs and self.device.type == "cuda"):
             return None
         shapes = ((batch, 4, 8, 8), (batch, 192), (batch,), (batch,), (batch,), (batch,))
         ent = self._graphs.get((tuple(torch.Size(s) for s in shapes), self.autocast_dtype, self.network.training))
@@ -500,15 +557,32 @@ class PPOAgent(BaseAgent):
         dev_stream = torch.cuda.current_stream(self.device)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(dev_stream)
+        world = _world()
         with torch.cuda.stream(side):
             for _ in range(3):
                 loss, _ = self._minibatch_loss(*static_in)
                 self._optimizer_step(loss)
+            # no autograd graph of the warm-up may outlive it: its AccumulateGrad nodes would be reused
+            # by the capture's backward and flagged as a stream mismatch
+            del loss
+        graphs = [torch.cuda.CUDAGraph()]
+        if world == 1:
+            with torch.cuda.graph(graphs[0], stream=side):
+                loss, stats = self._minibatch_loss(*static_in)
+                self._optimizer_step(loss)
+                del loss
+        else:
+            flat = self._grad_buffer()  # every .grad a view into it (made by the warm-up's eager steps)
+            graphs.append(torch.cuda.CUDAGraph())
+            with torch.cuda.graph(graphs[0], stream=side):
+                flat.zero_()
+                loss, stats = self._minibatch_loss(*static_in)
+                loss.backward()
+                del loss
+            with torch.cuda.graph(graphs[1], stream=side, pool=graphs[0].pool()):
+                flat.div_(world)
+                self._clip_and_step()
         dev_stream.wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            loss, stats = self._minibatch_loss(*static_in)
-            self._optimizer_step(loss)
         with torch.no_grad():
             for p, v in zip(self.network.parameters(), params):
                 p.copy_(v)
@@ -522,7 +596,7 @@ class PPOAgent(BaseAgent):
                             v.copy_(old[k])
                         else:  # fresh Adam state == zero moments at step 0
                             v.zero_()
-        return graph, static_in, stats
+        return graphs, static_in, stats
 
     def update(self, buffer, last_values, batch_size: Optional[int] = None) -> Dict[str, float]:
         """ppo.py:330-423.  Metrics are accumulated on the device and read once.
@@ -535,6 +609,7 @@ class PPOAgent(BaseAgent):
         buffer.compute_returns_and_advantages(last_values, cfg.gamma, cfg.gae_lambda)
         acc = torch.zeros(6, dtype=torch.float32, device=self.device)
         n = 0
+        self.minibatch_stats = []
         packed = hasattr(buffer, "get_minibatches")
         for _ in range(cfg.num_epochs):
             batches = buffer.get_minibatches(bs, out=self.minibatch_inputs) if packed else buffer.get_samples(bs)
@@ -545,7 +620,12 @@ class PPOAgent(BaseAgent):
                     boards, pieces, masks, actions, old_lp, adv, ret = batch
                     x = BlockBlastNetwork.stack_input(boards.to(self.device), pieces.to(self.device))
                     masks, actions, old_lp, adv, ret = (t.to(self.device) for t in (masks, actions, old_lp, adv, ret))
-                acc += self.train_minibatch(x, masks, actions, old_lp, adv, ret)
+                st = self.train_minibatch(x, masks, actions, old_lp, adv, ret)
+                acc += st
+                if self.record_minibatch_stats:  # a replayed step rewrites its stats tensor: keep a copy
+                    self.minibatch_stats.append(st.clone())
+                if self.minibatch_callback is not None:
+                    self.minibatch_callback(n, st)
                 n += 1
         m = (acc / max(n, 1)).tolist()
         keys = ("policy_loss", "value_loss", "entropy", "total_loss", "approx_kl", "clip_fraction")
@@ -575,6 +655,7 @@ class PPOAgent(BaseAgent):
                 if "step" in st and torch.is_tensor(st["step"]):
                     st["step"] = st["step"].to(self.device if cap else "cpu", torch.float32)
         self._graphs = {}  # captured graphs reference the replaced optimizer state
+        self.graph_epoch += 1
         if "config" in ckpt:
             self.config = PPOConfig.from_dict(ckpt["config"])
         self._flat_grad = None

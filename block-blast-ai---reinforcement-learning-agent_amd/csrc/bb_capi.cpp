@@ -162,8 +162,9 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
   if (getenv("BB_LANE_BUDGET") && !getenv("BB_LANE_QUICK")) e->lane_quick = 0;  // explicit budget mode
   if (const char* s = getenv("BB_PACK_FIRST")) e->pack_first = atoi(s) > 0 ? atoi(s) : 1;
   if (const char* s = getenv("BB_PACK_NEXT")) e->pack_next = atoi(s) > 0 ? atoi(s) : 0;
-  if (e->dbg || getenv("BB_LANE_BUDGET") || getenv("BB_LANE_QUICK")) e->fused_step = false;
   if (const char* s = getenv("BB_STEP_KERNELS")) e->fused_step = atoi(s) != 2;
+  // the diagnostic modes and lane knobs exist only on the step + escalate kernels: they always win
+  if (e->dbg || getenv("BB_LANE_BUDGET") || getenv("BB_LANE_QUICK")) e->fused_step = false;
   const size_t bytes = slab_bytes(num_envs);
   st = hipMalloc(&e->slab, bytes);
   if (st != hipSuccess) {
@@ -296,6 +297,8 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.policy_seed = out->policy_seed;
   a.policy_step = out->policy_step;
   a.env_offset = out->env_offset;
+  a.final_score = out->final_score;
+  a.final_moves = out->final_moves;
   DeviceGuard g(env->device);
   if (env->broken) return broken_fail(env, "bb_step");
   hipError_t st;
@@ -313,6 +316,8 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
     r.policy_step0 = out->policy_step - 1;  // step 0's next action uses policy_step0 + 1
     r.info = out->info;
     r.reward_f64 = out->reward_f64;
+    r.final_score = out->final_score;
+    r.final_moves = out->final_moves;
     st = launch_rollout(env->d, env->d_rows, env->d_dtab, a, r, (hipStream_t)stream);
   } else {
     st = launch_step(env->d, env->d_rows, env->d_dtab, d_actions, a, (hipStream_t)stream);

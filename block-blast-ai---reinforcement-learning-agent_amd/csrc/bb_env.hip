@@ -334,6 +334,10 @@ __device__ __forceinline__ void finalize(const Tables& t, const EnvDev& e, StepC
   a.terminated[i] = term ? 1 : 0;
   if (a.reward_f64) a.reward_f64[i] = rew;
   if (a.lines) a.lines[i] = (uint8_t)s.lines;
+  if (term) {  // info['final_score'] / info['moves'] of the ending episode (wrappers.py:97-101)
+    if (a.final_score) a.final_score[i] = s.score;
+    if (a.final_moves) a.final_moves[i] = s.moves;
+  }
 
   const uint64_t F3 = fprof ? __builtin_amdgcn_s_memtime() : 0;
   if (term && a.autoreset) {
@@ -669,7 +673,10 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 
 // kStepOut: the bb_step outputs (info record, fp64 reward) are written too --
 // the instantiation bb_step uses at T = 1; the rollout path runs without them.
-template <bool kStepOut>
+// kSingle: one step per launch (bb_step): the seeded-reset state is read and
+// expanded only by the envs that terminate, and only the state columns the
+// step changed are written back.
+template <bool kStepOut, bool kSingle>
 __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a, RollArgs r) {
   __shared__ Tables t;
@@ -682,8 +689,14 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   const int i = wave * kRollEnvs + (lane % kRollEnvs);
   const bool live = i < e.n;
   const bool primary = live && half == 0;
+  // bb_step (kSingle, T = 1): the seeded-reset state (seed words, has_seed) is read only by the envs
+  // that terminate, instead of being loaded and expanded into a post-reset hand by every env up front
+  constexpr bool lazy_reset = kSingle;
   StepCtx s;
+  s.seed_hi = s.seed_lo = 0ull;
+  s.has_seed = false;
   int act = 0;
+  // the action mask is recomputed by every step from board + hand: the stored column is never read
   uint64_t m[3] = {0ull, 0ull, 0ull};
   if (live) {
     s.i = i;
@@ -702,13 +715,15 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     s.rng.buf = e.rng_buf[i];
     s.rng.inc_hi = e.inc_hi[i];
     s.rng.inc_lo = e.inc_lo[i];
-    s.seed_hi = e.seed_hi[i];
-    s.seed_lo = e.seed_lo[i];
-    s.has_seed = e.has_seed[i] != 0;
-    m[0] = e.mask[3 * i + 0];
-    m[1] = e.mask[3 * i + 1];
-    m[2] = e.mask[3 * i + 2];
+    if (!lazy_reset) {
+      s.seed_hi = e.seed_hi[i];
+      s.seed_lo = e.seed_lo[i];
+      s.has_seed = e.has_seed[i] != 0;
+    }
   }
+  // loaded values: a single step's final stores skip the columns it left unchanged
+  StepCtx s0;
+  if constexpr (kSingle) s0 = s;
   // The two waves on a SIMD issue by priority, then age: the older one runs
   // nearly unimpeded and the younger one finishes up to 1.3x later, which
   // sets the launch time.  Partners (same workgroup, same SIMD) publish their
@@ -734,9 +749,11 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   Pcg rs = s.rng;
   uint32_t r_hand = 0;
   uint64_t rm[3] = {0ull, 0ull, 0ull};
-  if (live && s.has_seed) {
-    uint64_t B0;
-    reset_lane(t, true, s.seed_hi, s.seed_lo, rs, B0, r_hand, rm);
+  if constexpr (!kSingle) {
+    if (live && s.has_seed) {
+      uint64_t B0;
+      reset_lane(t, true, s.seed_hi, s.seed_lo, rs, B0, r_hand, rm);
+    }
   }
   const size_t N = (size_t)e.n;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3  // timing diagnostics: per-wave phase cycles (reference semantics)
@@ -924,8 +941,19 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
           r.info[o] = inf;
         }
       }
+      if (term && primary) {  // info['final_score'] / info['moves'] of the ending episode (wrappers.py:97-101)
+        if (r.final_score) r.final_score[o] = s.score;
+        if (r.final_moves) r.final_moves[o] = s.moves;
+      }
       if (term && a.autoreset) {  // wrappers.py:97-102
-        if (s.has_seed) {
+        if constexpr (lazy_reset) {
+          s.has_seed = e.has_seed[i] != 0;
+          if (s.has_seed) {
+            s.seed_hi = e.seed_hi[i];
+            s.seed_lo = e.seed_lo[i];
+          }
+          reset_lane(t, s.has_seed, s.seed_hi, s.seed_lo, s.rng, s.B, s.hand, m);
+        } else if (s.has_seed) {
           s.B = 0ull;
           s.hand = r_hand;
           s.rng.hi = rs.hi;
@@ -965,7 +993,22 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   if (lane == 0 && a.dbg_out)
     for (int q = 0; q < 18; ++q) a.dbg_out[18 * wave + q] = dg[q];
 #endif
-  if (primary) {
+  if (primary && kSingle) {  // only the columns that changed (a bb_step leaves most of rng / combo / lines alone)
+    if (s.B != s0.B) e.board[i] = s.B;
+    if (s.hand != s0.hand) e.hand[i] = s.hand;
+    if (s.rng.hi != s0.rng.hi || s.rng.lo != s0.rng.lo) {
+      e.rng_hi[i] = s.rng.hi;
+      e.rng_lo[i] = s.rng.lo;
+    }
+    if (s.rng.buf != s0.rng.buf) e.rng_buf[i] = s.rng.buf;
+    if (s.score != s0.score) e.score[i] = s.score;
+    if (s.combo != s0.combo) e.combo[i] = s.combo;
+    if (s.max_combo != s0.max_combo) e.max_combo[i] = s.max_combo;
+    if (s.moves != s0.moves) e.moves[i] = s.moves;
+    if (s.lines_tot != s0.lines_tot) e.lines[i] = s.lines_tot;
+    if (s.blocks != s0.blocks) e.blocks[i] = s.blocks;
+    if (s.prev != s0.prev) e.prev[i] = (uint16_t)s.prev;
+  } else if (primary) {
     e.board[i] = s.B;
     e.hand[i] = s.hand;
     e.rng_hi[i] = s.rng.hi;
@@ -978,6 +1021,8 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     e.lines[i] = s.lines_tot;
     e.blocks[i] = s.blocks;
     e.prev[i] = (uint16_t)s.prev;
+  }
+  if (primary) {
     e.mask[3 * i + 0] = m[0];
     e.mask[3 * i + 1] = m[1];
     e.mask[3 * i + 2] = m[2];
@@ -1104,10 +1149,17 @@ hipError_t launch_rollout(const EnvDev& e, const PieceRow* rows, const uint8_t* 
                           const RollArgs& r, hipStream_t s) {
   const int64_t waves = ((int64_t)e.n + kRollEnvs - 1) / kRollEnvs;
   const int64_t blocks = (waves * 64 + kRollBlock - 1) / kRollBlock;
-  if (r.info || r.reward_f64)
-    hipLaunchKernelGGL(rollout_kernel<true>, dim3((unsigned)blocks), dim3(kRollBlock), 0, s, e, rows, d, a, r);
-  else
-    hipLaunchKernelGGL(rollout_kernel<false>, dim3((unsigned)blocks), dim3(kRollBlock), 0, s, e, rows, d, a, r);
+  const dim3 g((unsigned)blocks), b(kRollBlock);
+  if (r.steps == 1) {  // bb_step
+    if (r.info || r.reward_f64)
+      hipLaunchKernelGGL((rollout_kernel<true, true>), g, b, 0, s, e, rows, d, a, r);
+    else
+      hipLaunchKernelGGL((rollout_kernel<false, true>), g, b, 0, s, e, rows, d, a, r);
+  } else if (r.info || r.reward_f64) {
+    hipLaunchKernelGGL((rollout_kernel<true, false>), g, b, 0, s, e, rows, d, a, r);
+  } else {
+    hipLaunchKernelGGL((rollout_kernel<false, false>), g, b, 0, s, e, rows, d, a, r);
+  }
   return hipGetLastError();
 }
 

@@ -58,6 +58,8 @@ struct StepArgs {
   uint64_t policy_seed;
   uint64_t policy_step;
   uint64_t env_offset;
+  int64_t* final_score;  // [N] optional: score of the envs that terminated (before the auto-reset)
+  int32_t* final_moves;  // [N] optional: their moves
 };
 
 // bb_rollout: T fused steps (see rollout_kernel).  Per-step outputs are [T][N].
@@ -73,6 +75,8 @@ struct RollArgs {
   uint64_t policy_step0;        // step t's next action uses policy_step0 + t + 1
   bb_info* info;                // [T][N] optional: bb_step's info record (bb_step through this kernel, T = 1)
   double* reward_f64;           // [T][N] optional: the fp64 reward
+  int64_t* final_score;         // [T][N] optional: written where the env terminated at step t (pre-reset score)
+  int32_t* final_moves;         // [T][N] optional: likewise its moves
 };
 
 hipError_t launch_reset(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const uint8_t* sel, hipStream_t s);

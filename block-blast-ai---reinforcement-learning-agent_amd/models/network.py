@@ -62,6 +62,7 @@ HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs
 HIP_CONV_IN = os.environ.get("BB_HIP_CONV_IN", "0") == "1"
 NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
 FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"  # bf16 Linear weights/biases cast in one launch each way
+CAST_PERM_ROW_MAX = 8192  # bb_cast_multi's permuted-row limit (perm_c * perm_hw, include/bbvec.h)
 LINEAR_RELU = os.environ.get("BB_LINEAR_RELU", "1") != "0"  # bf16 Linear -> ReLU: the ReLU in the GEMM epilogue
 PREP_MULTI = os.environ.get("BB_PREP_MULTI", "1") != "0"  # the HIP convs' weight images in one launch
 RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass
@@ -225,6 +226,8 @@ class BlockBlastNetwork(nn.Module):
         if not (FUSED_CASTS and h.is_cuda and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") == torch.bfloat16):
             return None
+        if perm0 is not None and perm0[0] * perm0[1] > CAST_PERM_ROW_MAX:
+            return None  # bb_cast_multi permutes one row per workgroup through LDS: autocast's path instead
         lins = self._linears()
         params, perms, slots = [], [], []
         for m in lins:

@@ -145,10 +145,17 @@ class DeviceEnvBatch:
         policy_seed: int = 0xB10C,
         policy_step: int = 0,
         mask_out: Optional[torch.Tensor] = None,
+        final_score: Optional[torch.Tensor] = None,
+        final_moves: Optional[torch.Tensor] = None,
     ) -> None:
         """actions: int32 [N] on this device.  Outputs land in self.reward /
-        self.terminated (+ reward_f64 / lines / info when requested)."""
+        self.terminated (+ reward_f64 / lines / info when requested).
+        final_score (int64 [N]) / final_moves (int32 [N]) receive the score and
+        moves of the envs that terminated (info['final_score'] / info['moves'])
+        and are left untouched elsewhere."""
         assert actions.dtype == torch.int32 and actions.is_cuda and actions.numel() == self.num_envs
+        for t, dt in ((final_score, torch.int64), (final_moves, torch.int32)):
+            assert t is None or (t.dtype == dt and t.is_cuda and t.is_contiguous() and t.numel() == self.num_envs)
         o = self._out
         o.reward = self.reward.data_ptr()
         o.terminated = self.terminated.data_ptr()
@@ -160,6 +167,8 @@ class DeviceEnvBatch:
         o.policy_seed = policy_seed
         o.policy_step = policy_step
         o.env_offset = self.env_offset
+        o.final_score = final_score.data_ptr() if final_score is not None else None
+        o.final_moves = final_moves.data_ptr() if final_moves is not None else None
         L.check(self.lib.bb_step(self.handle, _ptr(actions), C.byref(o), _stream(self.device)), "bb_step",
                 self.handle)
 

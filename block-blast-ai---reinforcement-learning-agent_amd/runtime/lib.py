@@ -55,6 +55,7 @@ class Info(C.Structure):
     ]
 
 
+ABI_VERSION = 2  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -70,6 +71,8 @@ class StepOut(C.Structure):
         ("policy_seed", C.c_uint64),
         ("policy_step", C.c_uint64),
         ("env_offset", C.c_uint64),
+        ("final_score", C.c_void_p),
+        ("final_moves", C.c_void_p),
     ]
 
 
@@ -179,8 +182,11 @@ def load(path: str | None = None):
             fn = getattr(lib, name)  # AttributeError == missing export
             fn.restype = res
             fn.argtypes = args
-        if lib.bb_abi_version() != 1:
-            raise BBNativeError("libbbvec ABI version mismatch")
+        v = lib.bb_abi_version()
+        # an A/B arm built from an earlier revision (BBVEC_LIB, tools/build_prev.sh) may be ABI 1: version 2
+        # only appended bb_step_out fields, which such a library never reads
+        if v != ABI_VERSION and not (os.environ.get("BBVEC_LIB") and v == 1):
+            raise BBNativeError(f"libbbvec ABI version mismatch ({v}, expected {ABI_VERSION})")
         if path is None:
             _lib = lib
         return lib

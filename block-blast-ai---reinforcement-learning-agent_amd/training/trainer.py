@@ -115,11 +115,12 @@ class DeviceRollout:
         self.x = torch.zeros((num_envs, 4, 8, 8), dtype=torch.float32, device=device)
         self.mask_bits = torch.zeros((num_envs, 3), dtype=torch.int64, device=device)
         self.actions32 = torch.zeros(num_envs, dtype=torch.int32, device=device)
-        # final score / moves of episodes ending at (t, i); valid where dones[t, i] == 1
+        # final score / moves of episodes ending at (t, i); valid where dones[t, i] == 1 (stale elsewhere)
         self.ep_score = torch.zeros((rollout_steps, num_envs), dtype=torch.int64, device=device)
         self.ep_moves = torch.zeros((rollout_steps, num_envs), dtype=torch.int32, device=device)
         self._graph = None          # captured rollout (collect(graph=True))
         self._graph_warm = False
+        self._graph_key = None      # (agent, agent.graph_epoch, train mode) the graph was captured for
         self._step_base = None
 
     def reset(self) -> None:
@@ -139,6 +140,9 @@ class DeviceRollout:
         if not graph or not self.env.device.type == "cuda":
             self._collect_steps(agent)
             return
+        key = (id(agent), agent.graph_epoch, agent.network.training)
+        if self._graph_key != key:  # new agent, parameter storage, layout, precision or mode: recapture
+            self._graph, self._graph_warm, self._graph_key = None, False, key
         if self._graph is None and not self._graph_warm:
             self._collect_steps(agent)  # eager warm-up: library algorithm selection, workspaces
             self._graph_warm = True
@@ -157,8 +161,6 @@ class DeviceRollout:
     def _collect_steps(self, agent: PPOAgent, step_base: Optional[torch.Tensor] = None) -> None:
         buf, env = self.buffer, self.env
         buf.reset()
-        info64 = env.info.view(torch.int64).view(self.n, 7)
-        info32 = env.info.view(torch.int32).view(self.n, 14)
         for t in range(self.T):
             env.snapshot(board=buf.board[t], hand=buf.hand[t], mask_bits=buf.mask_bits[t])
             a, lp, v = agent.act_device(self.x, buf.mask_bits[t], env_offset=self.offset, step_base=step_base,
@@ -167,11 +169,11 @@ class DeviceRollout:
             buf.log_probs[t].copy_(lp)
             buf.values[t].copy_(v)
             self.actions32.copy_(a)
-            env.step(self.actions32, want_info=True)
+            # final score / moves written by bb_step straight into row t for the envs that ended (the
+            # reference reads info['final_score'] / info['moves'] of terminated envs only, train.py:196-201)
+            env.step(self.actions32, final_score=self.ep_score[t], final_moves=self.ep_moves[t])
             buf.rewards[t].copy_(env.reward)
             buf.dones[t].copy_(env.terminated)
-            self.ep_score[t].copy_(info64[:, 0])   # bb_info.score: final score on termination
-            self.ep_moves[t].copy_(info32[:, 6])   # bb_info.moves
             env.obs(x=self.x)
             buf.advance()
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 1
+#define BB_ABI_VERSION 2  /* 2: bb_step_out.final_score / final_moves */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -93,6 +93,11 @@ typedef struct bb_step_out {
   uint64_t policy_seed;
   uint64_t policy_step;
   uint64_t env_offset;    /* global index of env 0 (multi-GPU shards)            */
+  int64_t* final_score;   /* [N] optional: written ONLY for envs that terminated:
+                             the episode's score before the auto-reset
+                             (info['final_score'], wrappers.py:97-101)          */
+  int32_t* final_moves;   /* [N] optional: likewise its moves (info['moves'];
+                             scripts/train.py:196-201 reads both)               */
 } bb_step_out;
 
 /* Host view of the packed per-env state (bb_get_state / bb_set_state).

@@ -486,6 +486,8 @@ static void env_reset(Env* e, uint64_t* hist) { /* block_blast_env.py:195-222 */
 typedef struct {
   double reward;
   int terminated, lines, invalid;
+  int64_t score; /* info['score'] / info['moves'] after the move, before any auto-reset */
+  int moves;
 } StepOut;
 
 /* block_blast_env.py:224-264 + the vec-env auto-reset of wrappers.py:97-102. */
@@ -494,6 +496,8 @@ static void env_step(const bbo_vec* v, Env* e, int action, StepOut* o, uint64_t*
   MoveResult res;
   o->lines = 0;
   o->invalid = 0;
+  o->score = e->eng.score;
+  o->moves = e->eng.moves;
   if (action < 0 || !make_move(&e->eng, p, r, c, &res, hist)) { /* block_blast_env.py:240-245 */
     o->reward = -10.0;
     o->terminated = 0;
@@ -503,6 +507,8 @@ static void env_step(const bbo_vec* v, Env* e, int action, StepOut* o, uint64_t*
   o->reward = env_reward(v, e, &res);
   o->terminated = res.game_over;
   o->lines = res.lines_cleared;
+  o->score = e->eng.score; /* wrappers.py:97-101: final_score = info['score'], read before env.reset() */
+  o->moves = e->eng.moves;
   if (o->terminated && v->autoreset) env_reset(e, hist);
 }
 
@@ -678,6 +684,42 @@ void bbo_rollout(bbo_vec* v, int T, int32_t* act_io, uint64_t policy_seed, uint6
       a = policy_action(m, philox_w0(policy_seed, env_offset + (uint64_t)i, policy_step0 + (uint64_t)t + 1));
     }
     act_io[i] = a;
+  }
+}
+
+static uint32_t hand_word(const Engine* g) {
+  return (uint32_t)g->hand[0] | ((uint32_t)g->hand[1] << 6) | ((uint32_t)g->hand[2] << 12) |
+         ((uint32_t)g->used[0] << 18) | ((uint32_t)g->used[1] << 19) | ((uint32_t)g->used[2] << 20) |
+         ((uint32_t)g->over << 21) | ((uint32_t)g->rng.has << 22);
+}
+
+/* Replay of a training rollout (scripts/train.py:173-203): T vec steps with
+ * recorded actions [T][n].  Per (t, i): the pre-step state snapshot (board
+ * bits, packed hand word, mask bits -- what the rollout buffer stores before
+ * the step), the step's f32 reward and terminated flag, and on termination the
+ * episode's final score and moves (info['final_score'] / info['moves'],
+ * wrappers.py:97-101; 0 elsewhere).  Any output may be NULL. */
+void bbo_replay(bbo_vec* v, int T, const int32_t* actions, uint64_t* board, uint32_t* hand, uint64_t* mask,
+                float* reward, uint8_t* term, int64_t* ep_score, int32_t* ep_moves, int threads) {
+  const int nt = set_threads(threads);
+  uint64_t* H = thread_hist(v, nt);
+  const size_t n = (size_t)v->n;
+#pragma omp parallel for num_threads(nt) schedule(dynamic, 16)
+  for (int i = 0; i < v->n; ++i) {
+    uint64_t* hist = H + (size_t)my_thread() * (MAX_ATTEMPTS + 1);
+    Env* e = &v->envs[i];
+    for (int t = 0; t < T; ++t) {
+      const size_t k = (size_t)t * n + (size_t)i;
+      if (board) board[k] = grid_bits(&e->eng.board);
+      if (hand) hand[k] = hand_word(&e->eng);
+      if (mask) action_mask(&e->eng, &mask[3 * k]);
+      StepOut o;
+      env_step(v, e, actions[k], &o, hist);
+      if (reward) reward[k] = (float)o.reward;
+      if (term) term[k] = (uint8_t)o.terminated;
+      if (ep_score) ep_score[k] = o.terminated ? o.score : 0;
+      if (ep_moves) ep_moves[k] = o.terminated ? o.moves : 0;
+    }
   }
 }
 

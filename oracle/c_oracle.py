@@ -24,9 +24,16 @@ def load():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
+            import subprocess
+
             from .build import build_oracle
 
-            build_oracle()
+            try:
+                build_oracle()
+            except (OSError, subprocess.CalledProcessError) as exc:  # no gcc / OpenMP here: the checker is absent
+                import pytest
+
+                pytest.skip(f"C oracle unavailable: {exc}")
         lib = C.CDLL(LIB_PATH)
         sig = {
             "bbo_abi_version": (C.c_int, []),
@@ -37,6 +44,7 @@ def load():
             "bbo_reset": (None, [_P, C.c_int]),
             "bbo_step": (None, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_int]),
             "bbo_rollout": (None, [_P, C.c_int, _P, _U64, _U64, _U64, _P, _P, _P, _P, _P, C.c_int]),
+            "bbo_replay": (None, [_P, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, C.c_int]),
             "bbo_random_actions": (None, [_P, C.c_int, _U64, _U64, _U64, _P]),
             "bbo_state": (None, [_P] + [_P] * 12),
             "bbo_set_board_hand": (None, [_P, _P, _P]),
@@ -141,6 +149,24 @@ class CVecEnv:
         self.lib.bbo_rollout(self.h, T, _p(act), policy_seed, policy_step0, env_offset, _p(out["reward"]),
                              _p(out["terminated"]), _p(out["lines"]), _p(out["actions"]), _p(out["mask"]), threads)
         out["next_action"] = act
+        return out
+
+    def replay(self, actions, threads=0):
+        """Step every env through recorded actions [T][N] (the training
+        rollout, scripts/train.py:173-203 with wrappers.py:75-116): returns the
+        pre-step snapshots (board bits, hand word, mask bits) and the outputs,
+        with the final score / moves of each episode ending at (t, i) (0
+        elsewhere; info['final_score'] / info['moves'], wrappers.py:97-101)."""
+        a = np.ascontiguousarray(actions, np.int32)
+        T, n = a.shape
+        assert n == self.n
+        out = {"board": np.zeros((T, n), np.uint64), "hand": np.zeros((T, n), np.uint32),
+               "mask": np.zeros((T, n, 3), np.uint64), "reward": np.zeros((T, n), np.float32),
+               "terminated": np.zeros((T, n), np.uint8), "ep_score": np.zeros((T, n), np.int64),
+               "ep_moves": np.zeros((T, n), np.int32)}
+        self.lib.bbo_replay(self.h, T, _p(a), _p(out["board"]), _p(out["hand"]), _p(out["mask"]),
+                            _p(out["reward"]), _p(out["terminated"]), _p(out["ep_score"]), _p(out["ep_moves"]),
+                            threads)
         return out
 
     def random_actions(self, mask, seed=0xB10C, step=0, env_offset=0):

@@ -71,7 +71,7 @@ def test_masked_sample_philox_uniform_and_distribution(cuda):
     assert np.abs(counts - p).max() < 0.01
 
 
-@pytest.mark.parametrize("T,N", [(128, 64), (128, 4096), (7, 3)])
+@pytest.mark.parametrize("T,N", [(128, 64), (128, 4096), (7, 3), (128, 65536)])  # (128, 65536): config 3
 def test_gae_bit_exact(cuda, T, N):
     from runtime import kernels as K
 

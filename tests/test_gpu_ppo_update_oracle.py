@@ -1,0 +1,231 @@
+"""The whole PPO update against the oracle's restatement.
+
+``PPOAgent.update`` on the GPU (fp32, the product path: bb_gae, advantage
+normalisation, minibatch gather, the HIP-graph-replayed optimizer step with the
+fused loss, HIP BatchNorm, MIOpen / hipBLASLt GEMMs, fused clip + Adam) is run
+on the same rollout as ``oracle.bb_ppo.ppo_update`` -- ppo.py:171-213
+(get_samples) and ppo.py:330-423 (update) restated on CPU float32 torch with
+the reference's plain modules -- from the same initial weights, with the same
+minibatch order per epoch and Dropout at 0 on both sides (its mask stream
+cannot be shared).  The rollout is config 1's shape (64 envs x 128 steps,
+batch 2048: four minibatches per epoch), recorded from the C oracle's envs
+under the synthetic policy, with old log-probs and values from the initial
+network.
+
+Checked: GAE advantages / returns bit-exact; normalised advantages within
+1e-6; every optimizer step's six statistics within 1e-5; the update's metric
+means within 1e-5; every step's clipped gradients within 1e-3 relative L2 per
+tensor; and every step's weight update within 1e-2 relative L2 per tensor and
+3e-5 per element (a tenth of one Adam step of lr = 3e-4).  The steps are
+compared from identical state: before each step the oracle loads the GPU's
+weights, BatchNorm buffers and Adam moments after the previous one (recorded
+through ``PPOAgent.minibatch_callback``).  Why these bounds: a convolution
+weight's gradient behind a BatchNorm is a sum of dy over the pixels where
+its input is 1, and BatchNorm makes dy sum to zero over all pixels, so small
+gradient elements are differences of large partial sums and carry fp32
+summation-order errors of a few percent of their own size (MIOpen's /
+hipBLASLt's order vs the CPU's); Adam's first steps normalise every gradient
+element to about +-lr, so such an element's update differs by that same
+fraction of lr (measured: up to 1.1e-5).  Free-running, these differences
+compound over the epochs to ~1e-3 of a minibatch loss, which says nothing
+about the pipeline's correctness.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import bb_ppo as OP
+from oracle import c_oracle as CO
+
+pytestmark = pytest.mark.gpu
+
+N_ENVS, T = 64, 128  # config 1 (default.yaml)
+POLICY_SEED = 0xB10C
+
+
+def _rollout(net: OP.ReferenceNetwork):
+    """64 C-oracle envs (seeds 42 + i) for 128 steps under the synthetic
+    policy; old log-probs and values from ``net`` (train mode, per step, as
+    scripts/train.py:177 with agent.train())."""
+    seeds = np.arange(42, 42 + N_ENVS, dtype=np.uint64)
+    tw = CO.CVecEnv(seeds)
+    tw.reset()
+    mask = tw.state()["mask"]
+    acts = []
+    for t in range(T):
+        a = tw.random_actions(mask, POLICY_SEED, t)
+        acts.append(a)
+        mask = tw.step(a)["mask"]
+    final = tw.state()
+    tw.close()
+    env = CO.CVecEnv(seeds)
+    env.reset()
+    rec = env.replay(np.stack(acts))
+    env.close()
+    boards, pieces, masks = OP.expand_packed(rec["board"], rec["hand"], rec["mask"])
+    fb, fp, _ = OP.expand_packed(final["board"], final["hand"], final["mask"])
+    m = copy.deepcopy(net).train()
+    logp = np.zeros((T, N_ENVS), np.float32)
+    vals = np.zeros((T, N_ENVS), np.float32)
+    act = np.stack(acts).astype(np.int64)
+    with torch.no_grad():
+        for t in range(T):
+            _, lp, _, v = m.get_action_and_value(torch.from_numpy(boards[t]), torch.from_numpy(pieces[t]),
+                                                 torch.from_numpy(masks[t]), torch.from_numpy(act[t]))
+            logp[t], vals[t] = lp.numpy(), v.numpy()
+        last = m(torch.from_numpy(fb), torch.from_numpy(fp))[1].numpy()
+    buf = {"boards": boards, "pieces": pieces, "action_masks": masks, "actions": act, "log_probs": logp,
+           "rewards": rec["reward"], "dones": rec["terminated"].astype(np.float32), "values": vals}
+    return buf, rec, last
+
+
+def _agent(net, cfg, cuda):
+    from agents import PPOAgent
+
+    agent = PPOAgent(cfg, device=cuda, sample_seed=1)
+    agent.network.load_state_dict(net.state_dict())
+    for mod in agent.network.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    agent.train()
+    agent.record_minibatch_stats = True
+    snaps = []
+
+    def snapshot(k, stats):  # the GPU's weights, buffers, clipped gradients and Adam state after step k
+        opt = agent.optimizer
+        adam = [{key: opt.state[p][key].detach().float().cpu().clone() for key in ("step", "exp_avg", "exp_avg_sq")}
+                for p in agent.network.parameters()]
+        sd = {key: v.detach().cpu().clone() for key, v in agent.network.state_dict().items()}
+        grads = {name: p.grad.detach().float().cpu().clone() for name, p in agent.network.named_parameters()
+                 if p.grad is not None}
+        snaps.append((sd, adam, grads))
+
+    agent.minibatch_callback = snapshot
+    return agent, snaps
+
+
+def _oracle_forced(net, buf, last, cfg, perm, snaps, per_gpu):
+    """oracle.bb_ppo.ppo_update where every optimizer step k > 0 starts from
+    the GPU's state after step k - 1 (weights, BatchNorm buffers, Adam
+    moments and step): each step is compared from identical state, so fp32
+    summation-order differences cannot compound through the epochs.  Returns
+    the oracle's metric means, per-step statistics and the largest weight
+    difference after any step."""
+    ref = copy.deepcopy(net)
+    opt = torch.optim.Adam(ref.parameters(), lr=cfg.learning_rate, eps=1e-5)
+    worst = {"update_abs": 0.0, "update_rel": 0.0, "grad_rel": 0.0}
+    start = {}
+
+    def before(k):
+        if k > 0:
+            sd, adam, _ = snaps[k - 1]
+            ref.load_state_dict(sd)
+            for p, st in zip(ref.parameters(), adam):
+                opt.state[p] = {key: v.clone() for key, v in st.items()}
+        start.update({name: p.detach().clone() for name, p in ref.named_parameters()})
+
+    def after(k, row):
+        np.testing.assert_allclose(np.asarray(row), per_gpu[k], rtol=1e-5, atol=1e-5, err_msg=f"step {k} stats")
+        sd, _, grads = snaps[k]
+        total = float(torch.sqrt(sum((p.grad.double() ** 2).sum() for p in ref.parameters() if p.grad is not None)))
+        for name, p in ref.named_parameters():
+            # a convolution bias feeding a BatchNorm has a true gradient of 0 (rounding noise on the CPU, 0 in
+            # the GPU's fp64 BatchNorm backward): relative checks only where a tensor carries real gradient
+            real = p.grad is not None and float(p.grad.norm()) > 1e-6 * total
+            if real and name in grads:  # clip_grad_norm_ scaled .grad in place on both sides
+                gr = float((grads[name] - p.grad).norm() / p.grad.norm())
+                worst["grad_rel"] = max(worst["grad_rel"], gr)
+                assert gr <= 1e-3, (k, name, "grad rel L2", gr)
+            d_ref = p.detach() - start[name]
+            d_gpu = sd[name].float() - start[name]
+            ab = float((d_gpu - d_ref).abs().max())
+            worst["update_abs"] = max(worst["update_abs"], ab)
+            assert ab <= 3e-5, (k, name, "update abs", ab)
+            if real:
+                rl = float((d_gpu - d_ref).norm() / d_ref.norm().clamp(min=1e-30))
+                worst["update_rel"] = max(worst["update_rel"], rl)
+                assert rl <= 1e-2, (k, name, "update rel L2", rl)
+
+    means, per, adv, ret = OP.ppo_update(ref, opt, buf, last, cfg, perm, before_step=before, after_step=after)
+    return means, per, adv, ret, worst
+
+
+def _check_means(means_gpu, means_ref):
+    for k in OP.STAT_KEYS:
+        assert abs(means_gpu[k] - means_ref[k]) <= 1e-5 * max(1.0, abs(means_ref[k])), k
+
+
+@pytest.fixture(scope="module")
+def setup():
+    torch.manual_seed(0)
+    net = OP.ReferenceNetwork(dropout=0.0)
+    buf, rec, last = _rollout(net)
+    return net, buf, rec, last
+
+
+def _cfg(epochs):
+    from agents import PPOConfig
+
+    return PPOConfig(batch_size=2048, num_epochs=epochs)
+
+
+def test_update_packed_matches_oracle(cuda, setup):
+    """PackedRolloutBuffer (the trainer's path) vs ppo_update, two epochs
+    (eight optimizer steps)."""
+    from agents.ppo import PackedRolloutBuffer
+
+    net, buf, rec, last = setup
+    cfg = _cfg(2)
+    perms = [np.random.default_rng(100 + e).permutation(T * N_ENVS) for e in range(cfg.num_epochs)]
+    agent, snaps = _agent(net, cfg, cuda)
+    pb = PackedRolloutBuffer(T, N_ENVS, cuda)
+    pb.board.copy_(torch.from_numpy(rec["board"].view(np.int64)))
+    pb.hand.copy_(torch.from_numpy(rec["hand"].view(np.int32)))
+    pb.mask_bits.copy_(torch.from_numpy(rec["mask"].view(np.int64)))
+    for k, dst in (("actions", pb.actions), ("log_probs", pb.log_probs), ("rewards", pb.rewards),
+                   ("dones", pb.dones), ("values", pb.values)):
+        dst.copy_(torch.from_numpy(buf[k]))
+    it = iter(perms)
+    pb.permutation = lambda total: next(it)
+    means_gpu = agent.update(pb, torch.from_numpy(last).to(cuda))
+    per_gpu = torch.stack(agent.minibatch_stats).double().cpu().numpy()
+    assert per_gpu.shape == (8, 6) and len(snaps) == 8
+
+    it_ref = iter(perms)
+    means_ref, per_ref, adv_ref, ret_ref, worst = _oracle_forced(net, buf, last, cfg, lambda total: next(it_ref),
+                                                                 snaps, per_gpu)
+    np.testing.assert_array_equal(pb.advantages.cpu().numpy(), adv_ref)  # GAE bit-exact
+    np.testing.assert_array_equal(pb.returns.cpu().numpy(), ret_ref)
+    np.testing.assert_allclose(pb.normalized_advantages().cpu().numpy(), OP.normalize_advantages(adv_ref),
+                               rtol=1e-6, atol=1e-6)
+    _check_means(means_gpu, means_ref)
+    print(f"packed update: {len(per_ref)} optimizer steps, stats max |diff| {np.abs(per_gpu - per_ref).max():.2e}, "
+          f"worst per step: update {worst['update_abs']:.2e} abs / {worst['update_rel']:.2e} rel L2, "
+          f"clipped gradient {worst['grad_rel']:.2e} rel L2")
+
+
+def test_update_reference_layout_matches_oracle(cuda, setup):
+    """RolloutBuffer in the reference's float32 layout, minibatch order from
+    numpy's global RandomState (ppo.py:199) seeded alike on both sides; one
+    epoch."""
+    from agents.ppo import RolloutBuffer
+
+    net, buf, rec, last = setup
+    cfg = _cfg(1)
+    agent, snaps = _agent(net, cfg, cuda)
+    rb = RolloutBuffer(T, N_ENVS, device=cuda)
+    for t in range(T):
+        rb.add(buf["boards"][t], buf["pieces"][t], buf["action_masks"][t], buf["actions"][t], buf["log_probs"][t],
+               buf["rewards"][t], buf["dones"][t], buf["values"][t])
+    np.random.seed(1234)
+    means_gpu = agent.update(rb, last)
+    per_gpu = torch.stack(agent.minibatch_stats).double().cpu().numpy()
+    np.random.seed(1234)
+    means_ref, per_ref, adv_ref, _, worst = _oracle_forced(net, buf, last, cfg, np.random.permutation, snaps, per_gpu)
+    np.testing.assert_array_equal(rb.advantages.cpu().numpy(), adv_ref)
+    _check_means(means_gpu, means_ref)
+    print(f"reference-layout update: stats max |diff| {np.abs(per_gpu - per_ref).max():.2e}, "
+          f"worst per step: update {worst['update_abs']:.2e} abs / {worst['update_rel']:.2e} rel L2, "
+          f"clipped gradient {worst['grad_rel']:.2e} rel L2")
