@@ -667,6 +667,17 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 #ifndef BB_ROLL_PHILOX_TOP
 #define BB_ROLL_PHILOX_TOP 0  // rollout: the policy uniform drawn at the top of every step (no branch)
 #endif
+#ifndef BB_STEP_LAZY_RESET
+#define BB_STEP_LAZY_RESET 1  // bb_step: seeded-reset state read and expanded only by terminating envs
+#endif
+#ifndef BB_STEP_COND_STORE
+// bb_step: 0 every state column written back; 1 only the columns that changed (measured: -2.5%, fewer bytes);
+// 2 the PCG64 columns only where the stream moved (a draw or a reset), the rest unconditionally
+#define BB_STEP_COND_STORE 2
+#endif
+#ifndef BB_ROLL_DRAW_EARLY
+#define BB_ROLL_DRAW_EARLY 0  // rollout: attempt 1 drawn before the move and quick-tested in every lane
+#endif
 #ifndef BB_ROLL_KSTEP
 #define BB_ROLL_KSTEP BB_ROLL_SLOTS  // copy c tests slots c * KSTEP, c * KSTEP + 1, ...
 #endif
@@ -691,7 +702,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   const bool primary = live && half == 0;
   // bb_step (kSingle, T = 1): the seeded-reset state (seed words, has_seed) is read only by the envs
   // that terminate, instead of being loaded and expanded into a post-reset hand by every env up front
-  constexpr bool lazy_reset = kSingle;
+  constexpr bool lazy_reset = kSingle && BB_STEP_LAZY_RESET;
   StepCtx s;
   s.seed_hi = s.seed_lo = 0ull;
   s.has_seed = false;
@@ -723,7 +734,8 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   }
   // loaded values: a single step's final stores skip the columns it left unchanged
   StepCtx s0;
-  if constexpr (kSingle) s0 = s;
+  if constexpr (kSingle && BB_STEP_COND_STORE == 1) s0 = s;
+  bool rng_moved = false;  // kSingle, BB_STEP_COND_STORE == 2: the stream advanced (a draw or a reset)
   // The two waves on a SIMD issue by priority, then age: the older one runs
   // nearly unimpeded and the younger one finishes up to 1.3x later, which
   // sets the launch time.  Partners (same workgroup, same SIMD) publish their
@@ -749,7 +761,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   Pcg rs = s.rng;
   uint32_t r_hand = 0;
   uint64_t rm[3] = {0ull, 0ull, 0ull};
-  if constexpr (!kSingle) {
+  if constexpr (!lazy_reset) {
     if (live && s.has_seed) {
       uint64_t B0;
       reset_lane(t, true, s.seed_hi, s.seed_lo, rs, B0, r_hand, rm);
@@ -800,6 +812,25 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     BB_DIAG_T(c0);
     bool park = false;
     Pcg after = s.rng;  // stream state after attempt 1's draws
+#if BB_ROLL_DRAW_EARLY && (!defined(BB_ROLL_DIAG) || BB_ROLL_DIAG == 3)
+    // attempt 1's three draws do not depend on the move: drawn before it with no branch, so the
+    // LCG multiplies overlap the move's table reads; the quick slot then runs in every lane (a wave
+    // of 32 envs nearly always has one whose move empties its hand) and counts only where it did
+    uint32_t ex0 = 0, ex1 = 0, ex2 = 0;
+    if (live) draw3(after, ex0, ex1, ex2);
+    if (live) {
+#if BB_ROLL_BFMOVE
+      const bool drew_now = apply_move_bf(t, s, act);
+#else
+      const bool drew_now = apply_move(t, s, act);
+#endif
+      const bool fits = quick_slot_bf(s.B, ex0, ex1, ex2, t.row, t.d, half * BB_ROLL_KSTEP);
+      if (drew_now) {
+        park = !fits;
+        s.hand = ex0 | (ex1 << 6) | (ex2 << 12);
+      }
+    }
+#else
     if (live) {
 #if BB_ROLL_BFMOVE
       const bool drew_now = apply_move_bf(t, s, act);
@@ -835,12 +866,14 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         s.hand = ids;
       }
     }
+#endif
     // accept if either copy accepted; else roll back for the wave search
     uint64_t acc = ~__ballot(park) & __ballot(live && s.drew);
     if (kRollEnvs < 64) acc |= (acc >> (kRollEnvs & 63)) | (acc << ((64 - kRollEnvs) & 63));  // every copy sees the others
     if (kRollEnvs == 16) acc |= (acc >> 32) | (acc << 32);
     const bool accepted = (acc >> lane) & 1ull;
     if (live && s.drew) {
+      rng_moved = true;
 #if !defined(BB_ROLL_DIAG) || BB_ROLL_DIAG == 3
       if (accepted) s.rng = after;
       park = !accepted;
@@ -946,6 +979,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         if (r.final_moves) r.final_moves[o] = s.moves;
       }
       if (term && a.autoreset) {  // wrappers.py:97-102
+        rng_moved = true;
         if constexpr (lazy_reset) {
           s.has_seed = e.has_seed[i] != 0;
           if (s.has_seed) {
@@ -993,7 +1027,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   if (lane == 0 && a.dbg_out)
     for (int q = 0; q < 18; ++q) a.dbg_out[18 * wave + q] = dg[q];
 #endif
-  if (primary && kSingle) {  // only the columns that changed (a bb_step leaves most of rng / combo / lines alone)
+  if (primary && kSingle && BB_STEP_COND_STORE == 1) {  // only the columns that changed (a bb_step leaves most of rng / combo / lines alone)
     if (s.B != s0.B) e.board[i] = s.B;
     if (s.hand != s0.hand) e.hand[i] = s.hand;
     if (s.rng.hi != s0.rng.hi || s.rng.lo != s0.rng.lo) {
@@ -1011,9 +1045,11 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   } else if (primary) {
     e.board[i] = s.B;
     e.hand[i] = s.hand;
-    e.rng_hi[i] = s.rng.hi;
-    e.rng_lo[i] = s.rng.lo;
-    e.rng_buf[i] = s.rng.buf;
+    if (!(kSingle && BB_STEP_COND_STORE == 2) || rng_moved) {
+      e.rng_hi[i] = s.rng.hi;
+      e.rng_lo[i] = s.rng.lo;
+      e.rng_buf[i] = s.rng.buf;
+    }
     e.score[i] = s.score;
     e.combo[i] = s.combo;
     e.max_combo[i] = s.max_combo;

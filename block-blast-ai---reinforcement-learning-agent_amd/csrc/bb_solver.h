@@ -564,6 +564,9 @@ constexpr int kMultiPasses = BB_MULTI_PASSES;
 #ifndef BB_PASS_BF
 #define BB_PASS_BF 1  // gen_hands_multi passes: slot decode + pair test without branches (pair_quick_bf)
 #endif
+#ifndef BB_PASS_OWNER_RL
+#define BB_PASS_OWNER_RL 0  // gen_hands_multi passes: slot owner by scalar reads of the attempt offsets (no LDS)
+#endif
 #ifndef BB_PASS_NC
 #define BB_PASS_NC 0  // 1: pass leaf tests without the line clear (pair_quick_nc; measured slower: more exact-phase work)
 #endif
@@ -885,6 +888,11 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       const int slot = base + lane;
       int j = 0;
       if (nb > 1) {
+#if BB_PASS_OWNER_RL
+        // owner = the number of packed attempt lanes after the first whose first slot is <= this one (their
+        // first slots ascend): one scalar read of each offset, no LDS round trip
+        for (int jj = 1; jj < nb; ++jj) j += slot >= __builtin_amdgcn_readlane(e_off, jj) ? 1 : 0;
+#else
         wave_lds_fence();
         lds[lane] = 0u;
         wave_lds_fence();
@@ -892,6 +900,7 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
           atomicMax(&lds[e_off > base ? e_off - base : 0], (uint32_t)lane);
         wave_lds_fence();
         j = (int)wave_incl_max(lds[lane]);
+#endif
       }
       const uint32_t jid = __shfl(e_ids, j);
       const uint64_t jA0 = __shfl(eA0, j), jA1 = __shfl(eA1, j), jA2 = __shfl(eA2, j);

@@ -5,11 +5,11 @@ import os
 import subprocess
 import sys
 
-from .lib import LIB_PATH, PKG_DIR, REPO_DIR
+from .lib import HOST_LIB_PATH, LIB_PATH, PKG_DIR, REPO_DIR
 
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_nn.hip", "bb_loss.hip", "bb_conv.hip", "bb_optim.hip", "bb_capi.cpp", "bb_tables.cpp"]
-HEADERS = ["bb_device.h", "bb_solver.h", "bb_env_internal.h"]
+HEADERS = ["bb_device.h", "bb_solver.h", "bb_env_internal.h", "bb_seed.h"]
 ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
 
 HIPCC_FLAGS = [
@@ -58,5 +58,27 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
     return LIB_PATH
 
 
+# the host backend of the env entry points (csrc/bb_host.cpp): plain C++, OpenMP over envs
+HOST_SOURCES = ["bb_host.cpp"]
+HOST_HEADERS = ["bb_seed.h"]
+HOST_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-fopenmp", "-Wall", "-Wextra"]
+
+
+def build_host_lib(force: bool = False, verbose: bool = True) -> str:
+    inputs = [os.path.join(CSRC, s) for s in HOST_SOURCES + HOST_HEADERS] + [
+        os.path.join(REPO_DIR, "include", "bbvec.h"), os.path.abspath(__file__)]
+    if not force and not _stale(HOST_LIB_PATH, inputs):
+        return HOST_LIB_PATH
+    tmp = HOST_LIB_PATH + ".tmp"
+    cmd = [os.environ.get("CXX", "g++"), *HOST_FLAGS, f"-I{os.path.join(REPO_DIR, 'include')}",
+           *[os.path.join(CSRC, s) for s in HOST_SOURCES], "-o", tmp]
+    if verbose:
+        print("[build]", " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, HOST_LIB_PATH)
+    return HOST_LIB_PATH
+
+
 if __name__ == "__main__":
     build_lib(force="--force" in sys.argv)
+    build_host_lib(force="--force" in sys.argv)

@@ -4,6 +4,10 @@ This is the torch-facing layer under the Gym surface.  All tensors live on the
 handle's GPU; every call launches on torch's current stream of that device and
 never synchronises (except the explicit host copies ``state()`` /
 ``set_state()``).
+
+``device="cpu"`` selects the host backend (libbbvec_host.so, the same C-ABI on
+CPU tensors, csrc/bb_host.cpp) explicitly; without it a missing HIP device is
+an error, never a silent switch to the CPU.
 """
 from __future__ import annotations
 
@@ -42,10 +46,14 @@ def _ptr(t: Optional[torch.Tensor]):
 
 
 def _stream(device: torch.device):
+    if device.type == "cpu":
+        return None
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
 def resolve_device(device=None) -> torch.device:
+    if device is not None and torch.device(device).type == "cpu":  # the host backend, asked for by name
+        return torch.device("cpu")
     if not torch.cuda.is_available():
         raise L.BBNativeError("no GPU visible to torch: the Block Blast env runs only on the HIP device")
     if device is None:
@@ -95,8 +103,8 @@ class DeviceEnvBatch:
         device=None,
         env_offset: int = 0,
     ):
-        self.lib = L.load()
         self.device = resolve_device(device)
+        self.lib = L.load_host() if self.device.type == "cpu" else L.load()
         self.num_envs = int(num_envs)
         self.env_offset = int(env_offset)
         rw = dict(DEFAULT_REWARDS)
@@ -105,9 +113,9 @@ class DeviceEnvBatch:
         self.reward_config = rw
         h = C.c_void_p()
         L.check(
-            self.lib.bb_create(self.num_envs, self.device.index, C.byref(L.reward_cfg(rw)), int(bool(autoreset)),
+            self.lib.bb_create(self.num_envs, self.device.index or 0, C.byref(L.reward_cfg(rw)), int(bool(autoreset)),
                                C.byref(h)),
-            "bb_create",
+            "bb_create", lib=self.lib,
         )
         self.handle = h
         dev = self.device
@@ -128,12 +136,12 @@ class DeviceEnvBatch:
         L.check(
             self.lib.bb_seed(self.handle, s.ctypes.data_as(C.c_void_p), has.ctypes.data_as(C.c_void_p),
                              raw.ctypes.data_as(C.c_void_p)),
-            "bb_seed", self.handle,
+            "bb_seed", self.handle, self.lib,
         )
 
     # --------------------------------------------------------------- hot path
     def reset(self, env_mask: Optional[torch.Tensor] = None) -> None:
-        L.check(self.lib.bb_reset(self.handle, _ptr(env_mask), _stream(self.device)), "bb_reset", self.handle)
+        L.check(self.lib.bb_reset(self.handle, _ptr(env_mask), _stream(self.device)), "bb_reset", self.handle, self.lib)
 
     def step(
         self,
@@ -153,9 +161,9 @@ class DeviceEnvBatch:
         final_score (int64 [N]) / final_moves (int32 [N]) receive the score and
         moves of the envs that terminated (info['final_score'] / info['moves'])
         and are left untouched elsewhere."""
-        assert actions.dtype == torch.int32 and actions.is_cuda and actions.numel() == self.num_envs
+        assert actions.dtype == torch.int32 and actions.device == self.device and actions.numel() == self.num_envs
         for t, dt in ((final_score, torch.int64), (final_moves, torch.int32)):
-            assert t is None or (t.dtype == dt and t.is_cuda and t.is_contiguous() and t.numel() == self.num_envs)
+            assert t is None or (t.dtype == dt and t.device == self.device and t.is_contiguous() and t.numel() == self.num_envs)
         o = self._out
         o.reward = self.reward.data_ptr()
         o.terminated = self.terminated.data_ptr()
@@ -170,7 +178,7 @@ class DeviceEnvBatch:
         o.final_score = final_score.data_ptr() if final_score is not None else None
         o.final_moves = final_moves.data_ptr() if final_moves is not None else None
         L.check(self.lib.bb_step(self.handle, _ptr(actions), C.byref(o), _stream(self.device)), "bb_step",
-                self.handle)
+                self.handle, self.lib)
 
     def rollout(
         self,
@@ -190,13 +198,13 @@ class DeviceEnvBatch:
         u8 / lines u8 / actions_out i32 are [steps, N], mask_out i64 [steps, N, 3].
         Equals ``steps`` chained ``step(..., next_action=, policy_step=policy_step0+t+1)``."""
         n = self.num_envs
-        assert actions.dtype == torch.int32 and actions.is_cuda and actions.numel() == n
+        assert actions.dtype == torch.int32 and actions.device == self.device and actions.numel() == n
         assert reward.dtype == torch.float32 and reward.numel() >= steps * n
         assert terminated.dtype == torch.uint8 and terminated.numel() >= steps * n
         for t, dt, per in ((lines, torch.uint8, 1), (actions_out, torch.int32, 1), (mask_out, torch.int64, 3),
                            (next_action, torch.int32, 0)):
             if t is not None:
-                assert t.dtype == dt and t.is_cuda and t.numel() >= (steps * n * per if per else n)
+                assert t.dtype == dt and t.device == self.device and t.numel() >= (steps * n * per if per else n)
         o = L.RolloutOut(reward=reward.data_ptr(), terminated=terminated.data_ptr(),
                          lines=lines.data_ptr() if lines is not None else None,
                          actions=actions_out.data_ptr() if actions_out is not None else None,
@@ -204,26 +212,26 @@ class DeviceEnvBatch:
                          next_action=next_action.data_ptr() if next_action is not None else None,
                          policy_seed=policy_seed, policy_step0=policy_step0, env_offset=self.env_offset)
         L.check(self.lib.bb_rollout(self.handle, int(steps), _ptr(actions), C.byref(o), _stream(self.device)),
-                "bb_rollout", self.handle)
+                "bb_rollout", self.handle, self.lib)
 
     def obs(self, x=None, mask_i8=None, mask_f32=None, mask_bits=None) -> None:
         L.check(
             self.lib.bb_obs(self.handle, _ptr(x), _ptr(mask_i8), _ptr(mask_f32), _ptr(mask_bits),
                             _stream(self.device)),
-            "bb_obs", self.handle,
+            "bb_obs", self.handle, self.lib,
         )
 
     def snapshot(self, board=None, hand=None, mask_bits=None) -> None:
         L.check(
             self.lib.bb_snapshot(self.handle, _ptr(board), _ptr(hand), _ptr(mask_bits), _stream(self.device)),
-            "bb_snapshot", self.handle,
+            "bb_snapshot", self.handle, self.lib,
         )
 
     def random_actions(self, mask_bits: torch.Tensor, out: torch.Tensor, seed: int = 0xB10C, step: int = 0):
         L.check(
             self.lib.bb_random_actions(_ptr(mask_bits), self.num_envs, seed, step, self.env_offset, _ptr(out),
                                        _stream(self.device)),
-            "bb_random_actions",
+            "bb_random_actions", None, self.lib,
         )
 
     # ------------------------------------------------------------ host copies
@@ -236,7 +244,7 @@ class DeviceEnvBatch:
             "prev_center": np.zeros(n, np.uint8), "rng": np.zeros((n, 3), np.uint64),
         }
         v = L.StateView(**{k: a.ctypes.data for k, a in out.items()})
-        L.check(self.lib.bb_get_state(self.handle, C.byref(v)), "bb_get_state", self.handle)
+        L.check(self.lib.bb_get_state(self.handle, C.byref(v)), "bb_get_state", self.handle, self.lib)
         return out
 
     def set_state(self, **arrays) -> None:
@@ -250,14 +258,15 @@ class DeviceEnvBatch:
             keep[k] = arr
             kw[k] = arr.ctypes.data
         v = L.StateView(**kw)
-        L.check(self.lib.bb_set_state(self.handle, C.byref(v)), "bb_set_state", self.handle)
+        L.check(self.lib.bb_set_state(self.handle, C.byref(v)), "bb_set_state", self.handle, self.lib)
 
     def info_host(self) -> np.ndarray:
         return self.info.cpu().numpy().view(INFO_DTYPE)
 
     def close(self) -> None:
         if getattr(self, "handle", None):
-            torch.cuda.synchronize(self.device)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
             self.lib.bb_destroy(self.handle)
             self.handle = None
 

@@ -3,6 +3,10 @@
 This is the only way the product reaches its kernels.  There is no CPU
 fallback: if the library is missing or no HIP device is present, the first
 call raises ``BBNativeError`` with the reason.
+
+``load_host()`` binds the env half of the same ABI from libbbvec_host.so, the
+host backend (csrc/bb_host.cpp) that ``DeviceEnvBatch(device="cpu")`` selects
+explicitly; nothing falls back to it.
 """
 from __future__ import annotations
 
@@ -13,6 +17,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.environ.get("BBVEC_LIB", os.path.join(PKG_DIR, "libbbvec.so"))
+HOST_LIB_PATH = os.path.join(PKG_DIR, "libbbvec_host.so")
 
 BB_OK = 0
 BB_ACTIONS = 192
@@ -161,7 +166,13 @@ SIGNATURES = {
     "bb_cast_multi": (C.c_int, [_I32, _I32, _P, _P, _P, _P, _P, _P]),
 }
 
+# the env entry points, which the host backend (libbbvec_host.so) exports too
+HOST_SYMBOLS = ("bb_abi_version", "bb_create", "bb_destroy", "bb_last_error", "bb_num_envs", "bb_pcg64_seed",
+                "bb_seed", "bb_reset", "bb_step", "bb_rollout", "bb_obs", "bb_device_ptrs", "bb_snapshot",
+                "bb_get_state", "bb_set_state", "bb_random_actions")
+
 _lib = None
+_host = None
 _lock = threading.Lock()
 
 
@@ -192,14 +203,35 @@ def load(path: str | None = None):
         return lib
 
 
-def last_error(handle=None) -> str:
-    msg = load().bb_last_error(handle)
+def load_host():
+    """Load libbbvec_host.so (once), the host backend of the env entry points."""
+    global _host
+    with _lock:
+        if _host is not None:
+            return _host
+        if not os.path.exists(HOST_LIB_PATH):
+            raise BBNativeError(f"host backend not found at {HOST_LIB_PATH}; build it with "
+                                "`python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = C.CDLL(HOST_LIB_PATH)
+        for name in HOST_SYMBOLS:
+            res, args = SIGNATURES[name]
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.bb_abi_version() != ABI_VERSION:
+            raise BBNativeError("libbbvec_host ABI version mismatch")
+        _host = lib
+        return lib
+
+
+def last_error(handle=None, lib=None) -> str:
+    msg = (lib or load()).bb_last_error(handle)
     return msg.decode() if msg else ""
 
 
-def check(rc: int, what: str, handle=None) -> None:
+def check(rc: int, what: str, handle=None, lib=None) -> None:
     if rc != BB_OK:
-        raise BBNativeError(f"{what} failed ({rc}): {last_error(handle)}")
+        raise BBNativeError(f"{what} failed ({rc}): {last_error(handle, lib)}")
 
 
 def pcg64_seed(seed: int):

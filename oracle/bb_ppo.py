@@ -210,17 +210,46 @@ def get_samples(buf: Dict[str, np.ndarray], batch_size: int, indices: np.ndarray
 STAT_KEYS = ("policy_loss", "value_loss", "entropy", "total_loss", "approx_kl", "clip_fraction")
 
 
+def minibatch_loss(network: ReferenceNetwork, batch, cfg):
+    """ppo.py:364-392: the clipped surrogate, MSE value loss and entropy bonus
+    of one minibatch (in the network's dtype)."""
+    boards, pieces, masks, actions, old_log_probs, advantages, returns = batch
+    dt = next(network.parameters()).dtype
+    boards, pieces, masks, old_log_probs, advantages, returns = (
+        t.to(dt) for t in (boards, pieces, masks, old_log_probs, advantages, returns))
+    _, new_log_probs, entropy, values = network.get_action_and_value(boards, pieces, masks, actions)
+    ratio = torch.exp(new_log_probs - old_log_probs)
+    surr1 = ratio * advantages
+    surr2 = torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon) * advantages
+    policy_loss = -torch.min(surr1, surr2).mean()
+    value_loss = F.mse_loss(values, returns)
+    entropy_loss = -entropy.mean()
+    loss = policy_loss + cfg.value_coef * value_loss + cfg.entropy_coef * entropy_loss
+    return policy_loss, value_loss, entropy, loss, ratio
+
+
+def clipped_grads(network: ReferenceNetwork, batch, cfg) -> Dict[str, torch.Tensor]:
+    """The minibatch's gradients after clip_grad_norm_(max_grad_norm)
+    (ppo.py:395-400) in the network's own dtype (tests run it in float64 as
+    the ground truth that fp32 implementations are measured against)."""
+    network.zero_grad(set_to_none=True)
+    minibatch_loss(network, batch, cfg)[3].backward()
+    nn.utils.clip_grad_norm_(network.parameters(), cfg.max_grad_norm)
+    return {n: p.grad.detach().clone() for n, p in network.named_parameters() if p.grad is not None}
+
+
 def ppo_update(network: ReferenceNetwork, optimizer: torch.optim.Optimizer, buf: Dict[str, np.ndarray],
                last_values: np.ndarray, cfg, permutation: Callable[[int], np.ndarray],
                before_step: Optional[Callable[[int], None]] = None,
-               after_step: Optional[Callable[[int, List[float]], None]] = None):
+               after_step: Optional[Callable[..., None]] = None):
     """PPOAgent.update (ppo.py:330-423) on a CPU float32 buffer in the
     reference's layout (boards, pieces, action_masks f32; actions i64;
     log_probs, rewards, dones, values f32; all [T, N, ...]).  ``cfg`` carries
     the PPOConfig fields; ``permutation(total)`` supplies each epoch's
     minibatch order; ``before_step(k)`` / ``after_step(k, stats)`` run around
     optimizer step k (tests load another implementation's state there, so each
-    step is compared from identical weights).  Returns (metric means, per-minibatch statistics [n, 6],
+    step is compared from identical weights; after_step also gets the
+    minibatch).  Returns (metric means, per-minibatch statistics [n, 6],
     advantages, returns)."""
     adv, ret = gae(buf["rewards"], buf["values"], buf["dones"], last_values, cfg.gamma, cfg.gae_lambda)
     buf = dict(buf, advantages=adv, returns=ret)
@@ -230,15 +259,7 @@ def ppo_update(network: ReferenceNetwork, optimizer: torch.optim.Optimizer, buf:
         for batch in get_samples(buf, cfg.batch_size, permutation(T * N)):
             if before_step is not None:
                 before_step(len(rows))
-            boards, pieces, masks, actions, old_log_probs, advantages, returns = batch
-            _, new_log_probs, entropy, values = network.get_action_and_value(boards, pieces, masks, actions)
-            ratio = torch.exp(new_log_probs - old_log_probs)
-            surr1 = ratio * advantages
-            surr2 = torch.clamp(ratio, 1 - cfg.clip_epsilon, 1 + cfg.clip_epsilon) * advantages
-            policy_loss = -torch.min(surr1, surr2).mean()
-            value_loss = F.mse_loss(values, returns)
-            entropy_loss = -entropy.mean()
-            loss = policy_loss + cfg.value_coef * value_loss + cfg.entropy_coef * entropy_loss
+            policy_loss, value_loss, entropy, loss, ratio = minibatch_loss(network, batch, cfg)
             optimizer.zero_grad()
             loss.backward()
             nn.utils.clip_grad_norm_(network.parameters(), cfg.max_grad_norm)
@@ -249,7 +270,7 @@ def ppo_update(network: ReferenceNetwork, optimizer: torch.optim.Optimizer, buf:
             rows.append([policy_loss.item(), value_loss.item(), entropy.mean().item(), loss.item(),
                          approx_kl.item(), clip_fraction.item()])
             if after_step is not None:
-                after_step(len(rows) - 1, rows[-1])
+                after_step(len(rows) - 1, rows[-1], batch)
     per = np.array(rows, dtype=np.float64).reshape(-1, 6)
     means = {k: sum(r[j] for r in rows) / max(len(rows), 1) for j, k in enumerate(STAT_KEYS)}  # ppo.py:408-423
     return means, per, adv, ret

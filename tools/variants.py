@@ -30,6 +30,15 @@ VARIANTS = {
     # rollout: branchy apply_move; policy Philox at the top of every step
     "brmove": ["-DBB_ROLL_BFMOVE=0"],
     "ptop": ["-DBB_ROLL_PHILOX_TOP=1"],
+    # rollout: attempt 1 drawn before the move, quick slot in every lane (no branch)
+    "dearly": ["-DBB_ROLL_DRAW_EARLY=1"],
+    # gen_hands_multi passes: slot owner by scalar reads of the attempt offsets instead of LDS markers
+    "ownrl": ["-DBB_PASS_OWNER_RL=1"],
+    # bb_step (single-step instantiation): eager seeded-reset state / unconditional column stores
+    "seager": ["-DBB_STEP_LAZY_RESET=0"],
+    "sallst": ["-DBB_STEP_COND_STORE=0"],
+    "scond1": ["-DBB_STEP_COND_STORE=1"],
+    "seager_allst": ["-DBB_STEP_LAZY_RESET=0", "-DBB_STEP_COND_STORE=0"],
     "brquick": ["-DBB_ROLL_BFQUICK=0"],
     "brpass": ["-DBB_PASS_BF=0"],
     # rollout SIMD-partner priority: 0 none, 1 alternate per step, 2 the wave behind takes it (shipped)
