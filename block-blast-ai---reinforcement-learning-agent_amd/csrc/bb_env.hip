@@ -102,6 +102,12 @@ __device__ __forceinline__ void stage_tables(Tables& t, const PieceRow* g_rows, 
   __syncthreads();
 }
 
+// Every lane gets lane (l mod 32)'s value: v_permlane32_swap(x, x) moves lanes 0-31 of the source into
+// lanes 32-63 of the destination and leaves lanes 0-31 in place.
+__device__ __forceinline__ uint32_t lower_half_bcast(uint32_t x) {
+  return __builtin_amdgcn_permlane32_swap(x, x, false, false)[0];
+}
+
 __device__ __forceinline__ void masks_of(const Tables& t, uint64_t B, uint32_t hand, uint64_t m[3]) {
   const uint32_t used = hand_used(hand);
 #pragma unroll
@@ -675,6 +681,11 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 // 2 the PCG64 columns only where the stream moved (a draw or a reset), the rest unconditionally
 #define BB_STEP_COND_STORE 2
 #endif
+#ifndef BB_ROLL_HALF_IDLE
+// rollout: copy 1 exec-masked off through the move and the finalize (its duplicate work there is
+// dropped; +0.8%, 8.87 vs 8.81e9 env-steps/s, 3 interleaved repeats, profiles/r03/ab/r03g_*)
+#define BB_ROLL_HALF_IDLE 1
+#endif
 #ifndef BB_ROLL_DRAW_EARLY
 #define BB_ROLL_DRAW_EARLY 0  // rollout: attempt 1 drawn before the move and quick-tested in every lane
 #endif
@@ -830,6 +841,29 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         s.hand = ex0 | (ex1 << 6) | (ex2 << 12);
       }
     }
+#elif BB_ROLL_HALF_IDLE && (!defined(BB_ROLL_DIAG) || BB_ROLL_DIAG == 3)
+    // copy 1 idles through the move (and the finalize below): it takes the post-move board and the
+    // drawn pieces from copy 0 (lane l -> l + 32, one v_permlane32_swap per dword) for its own
+    // quick-test slot, and joins the wave search, which reads every env from copy 0's lane
+    uint32_t ids0 = 0;
+    bool drew0 = false;
+    if (live && half == 0) {
+      drew0 = apply_move_bf(t, s, act);
+      if (drew0) {
+        const Pcg save = s.rng;
+        uint32_t x0, x1, x2;
+        draw3(s.rng, x0, x1, x2);
+        ids0 = x0 | (x1 << 6) | (x2 << 12);
+        after = s.rng;
+        s.rng = save;
+        s.hand = ids0;
+      }
+    }
+    const uint32_t idq = lower_half_bcast((uint32_t)ids0 | ((uint32_t)drew0 << 31));
+    const uint64_t Bq = ((uint64_t)lower_half_bcast((uint32_t)(s.B >> 32)) << 32) | lower_half_bcast((uint32_t)s.B);
+    if (live && (idq >> 31)) {
+      park = !quick_slot_bf(Bq, idq & 63u, (idq >> 6) & 63u, (idq >> 12) & 63u, t.row, t.d, half * BB_ROLL_KSTEP);
+    }
 #else
     if (live) {
 #if BB_ROLL_BFMOVE
@@ -868,11 +902,17 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     }
 #endif
     // accept if either copy accepted; else roll back for the wave search
+#if BB_ROLL_HALF_IDLE
+    uint64_t drew_bits = __ballot(live && half == 0 && s.drew);  // copy 1 did not move: copy 0's flags
+    drew_bits |= drew_bits << 32;
+    uint64_t acc = ~__ballot(park) & drew_bits;
+#else
     uint64_t acc = ~__ballot(park) & __ballot(live && s.drew);
+#endif
     if (kRollEnvs < 64) acc |= (acc >> (kRollEnvs & 63)) | (acc << ((64 - kRollEnvs) & 63));  // every copy sees the others
     if (kRollEnvs == 16) acc |= (acc >> 32) | (acc << 32);
     const bool accepted = (acc >> lane) & 1ull;
-    if (live && s.drew) {
+    if (live && s.drew && (!BB_ROLL_HALF_IDLE || half == 0)) {
       rng_moved = true;
 #if !defined(BB_ROLL_DIAG) || BB_ROLL_DIAG == 3
       if (accepted) s.rng = after;
@@ -932,7 +972,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + step + 1 + half);
     const uint32_t u_next = __shfl(u_drawn, (lane % kRollEnvs) + kRollEnvs * (step % kCopies));
 #endif
-    if (live) {
+    if (live && (!BB_ROLL_HALF_IDLE || half == 0)) {
       masks_of(t, s.B, s.hand, m);
       double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
       bool term = false;

@@ -34,6 +34,10 @@ VARIANTS = {
     "dearly": ["-DBB_ROLL_DRAW_EARLY=1"],
     # gen_hands_multi passes: slot owner by scalar reads of the attempt offsets instead of LDS markers
     "ownrl": ["-DBB_PASS_OWNER_RL=1"],
+    # rollout: copy 1 exec-masked off through the move and the finalize (board + drawn ids by permlane32_swap);
+    # shipped (r03), "halfoff" is the round-2 form with both copies doing the move and the finalize
+    "halfidle": ["-DBB_ROLL_HALF_IDLE=1"],
+    "halfoff": ["-DBB_ROLL_HALF_IDLE=0"],
     # bb_step (single-step instantiation): eager seeded-reset state / unconditional column stores
     "seager": ["-DBB_STEP_LAZY_RESET=0"],
     "sallst": ["-DBB_STEP_COND_STORE=0"],
