@@ -576,7 +576,7 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
   // packed into one pass (gen_hands_multi, as in rollout_kernel); the step
   // kernel's attempts count against each env's 100 (engine.py:159-172)
   if (!(a.dbg & 2)) {
-    gen_hands_multi<kEscGroup>(parked, s.B, s.rng, my_ids, t.row, t.d, J, lane, a.pack_first, a.pack_next,
+    gen_hands_multi<kEscGroup, true>(parked, s.B, s.rng, my_ids, t.row, t.d, J, lane, a.pack_first, a.pack_next,
                                scratch + (threadIdx.x & ~63), nullptr, (int)(pr & 0xFFu));
     if (flagged) {
       s.hand = my_ids | ((uint32_t)s.rng.has << 22);
@@ -928,10 +928,10 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       uint32_t ids = 0;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
       dg[3] += (uint64_t)__popcll(parked);
-      gen_hands_multi<kRollEnvs>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds,
+      gen_hands_multi<kRollEnvs, kSingle>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds,
                                  &dg[9]);
 #else
-      gen_hands_multi<kRollEnvs>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+      gen_hands_multi<kRollEnvs, kSingle>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
 #endif
       if ((parked >> (lane % kRollEnvs)) & 1ull) s.hand = ids | ((uint32_t)s.rng.has << 22);
     }

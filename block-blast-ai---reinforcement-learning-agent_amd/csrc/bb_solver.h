@@ -493,14 +493,71 @@ __device__ __forceinline__ void wave_lds_fence() {
 // task's owner slot is found by scattering each slot's first task index to
 // LDS and taking a prefix max (DPP).  Returns this lane's slot verdict.
 // lds: 64 words of wave-private LDS scratch.  All lanes call it.
+//
+// key (BB_SLOW_EXIT): env << 8 | attempt order of this lane's slot.  A success
+// decides its env's attempt, so it settles every slot of the same env at the
+// same or a later attempt (those verdicts can no longer change the earliest
+// success); the scan stops once every needed slot is settled or has had all
+// of its tasks.  An attempt that is solvable usually succeeds on its first
+// tasks, so this ends the flattened scan long before its last task.
+#ifndef BB_SLOW_EXIT
+#define BB_SLOW_EXIT 1
+#endif
+//
+// BB_SLOW_LINE_ONLY: one order's leaves suffice where the first placement
+// clears nothing.  If c at r completes no line and b then fits, b's anchor is
+// disjoint from c@r on B1, so placing b there first (a clear only frees cells)
+// leaves c@r legal: that b-first leaf succeeds too.  So every leaf of the order
+// whose first piece has fewer anchors is tested, and of the other order only
+// the first placements that complete a line.
+// The filter is a per-lane loop over anchors: it pays only for long task lists
+// (more than BB_SLOW_LINE_MIN tasks over the wave) and only where one long list
+// sets the launch time -- bb_step's single step (kLineOnly); in the rollout
+// kernel the same code measured -2% (its exact phases are short and the tail
+// averages out over the steps).
+#ifndef BB_SLOW_LINE_ONLY
+#define BB_SLOW_LINE_ONLY 1
+#endif
+#ifndef BB_SLOW_LINE_MIN
+#define BB_SLOW_LINE_MIN 512
+#endif
+template <bool kLineOnly = false>
 __device__ __forceinline__ bool slow_phase_wave(bool need, uint64_t B1, uint32_t bi, uint32_t ci, uint64_t A2,
-                                                uint64_t A3, const PieceRow* tbl, int lane, uint32_t* lds) {
+                                                uint64_t A3, const PieceRow* tbl, int lane, uint32_t* lds,
+                                                uint32_t key) {
+  if constexpr (kLineOnly && BB_SLOW_LINE_ONLY) {
+  const uint32_t all = need ? (uint32_t)(__popcll(A2) + __popcll(A3)) : 0u;
+  const uint32_t all_tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_add(all), 63);  // every lane
+  if (all_tot > (uint32_t)BB_SLOW_LINE_MIN && need) {
+    if (__popcll(A3) < __popcll(A2)) {  // c first in full, b first only where b completes a line
+      const uint32_t ti = bi;
+      bi = ci;
+      ci = ti;
+      const uint64_t tA = A2;
+      A2 = A3;
+      A3 = tA;
+    }
+    uint64_t line = 0ull;  // anchors of ci (second order's first piece) that complete a line on B1
+    if (A3 && line_within_reach(B1)) {
+      const uint64_t cs = tbl[ci].shape;
+      uint64_t x = A3;
+#pragma unroll 1
+      while (x) {
+        const uint64_t bit = x & (0ull - x);
+        x ^= bit;
+        if (has_full_line(B1 | (cs << (__ffsll((unsigned long long)bit) - 1)))) line |= bit;
+      }
+    }
+    A3 = line;
+  }
+  }
   const uint32_t n2 = need ? (uint32_t)__popcll(A2) : 0u;
   const uint32_t cnt = n2 + (need ? (uint32_t)__popcll(A3) : 0u);
   const uint32_t incl = wave_incl_add(cnt);
   const uint32_t off = incl - cnt;
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   uint64_t won_mask = 0ull;  // bit o: slot o has a successful leaf
+  uint64_t pending = __ballot(need);  // needed slots not settled yet
 #pragma unroll 1
   for (uint32_t base = 0; base < total; base += 64u) {
     // owner of task base+lane: the last slot whose first task is <= it
@@ -529,8 +586,17 @@ __device__ __forceinline__ bool slow_phase_wave(bool need, uint64_t B1, uint32_t
     while (hits) {
       const int l = __ffsll((unsigned long long)hits) - 1;
       hits &= hits - 1;
-      won_mask |= 1ull << __builtin_amdgcn_readlane(o, l);
+      const int ol = __builtin_amdgcn_readlane(o, l);
+      won_mask |= 1ull << ol;
+#if BB_SLOW_EXIT
+      const uint32_t ko = (uint32_t)__builtin_amdgcn_readlane((int)key, ol);
+      pending &= ~__ballot((key >> 8) == (ko >> 8) && (key & 0xFFu) >= (ko & 0xFFu));
+#endif
     }
+#if BB_SLOW_EXIT
+    pending &= ~__ballot(need && incl <= base + 64u);  // every task of the slot done
+    if (!pending) break;
+#endif
   }
   return (won_mask >> lane) & 1ull;
 }
@@ -735,7 +801,7 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
       if (needs) {
 #if BB_SLOW_FLAT
         const uint64_t tq2 = stats ? __builtin_amdgcn_s_memtime() : 0;
-        ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds);
+        ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds, (uint32_t)j);  // one env: attempt j
         uint64_t C2 = 0ull, C3 = 0ull;
 #else
         uint64_t C2 = 0ull, C3 = 0ull;
@@ -801,7 +867,7 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
 // packed (all failed) attempts.  The first attempt lane is always packed, so
 // every round makes progress.
 // ---------------------------------------------------------------------------
-template <int kEnvs>
+template <int kEnvs, bool kLineOnly = false>
 __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pcg& rng, uint32_t& ids,
                                                 const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
                                                 int lane, int pack_first, int pack_next, uint32_t* lds,
@@ -964,7 +1030,9 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       bool ok = q == 1;
       const bool need = q == 2 && !((qam | okm) & jenv & ((2ull << j) - 1ull));
       BB_MT(q1);
-      if (__ballot(need)) ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds);
+      if (__ballot(need))  // attempt lane j = env slot j % E, its attempt j / E
+        ok |= slow_phase_wave<kLineOnly>(need, B1, bi, ci, A2, A3, tbl, lane, lds,
+                                         (uint32_t)((j % E) << 8 | (j / E)));
       BB_MT(q2);
       pq += q1 - q0;
       ps += q2 - q1;

@@ -93,6 +93,18 @@ VARIANTS = {
     "bnr1024": ["-DBB_BN_RBLOCKS=1024"],
     "bnr2048": ["-DBB_BN_RBLOCKS=2048"],
     "cdiag2": ["-DBB_CONV_DIAG=2"],
+    # bb_step (T = 1) workgroup-cooperative hand search (tools/patches/step_coop.diff, measured slower and
+    # not shipped; apply the patch to rebuild these): off, own-search rounds first, attempts per wave and round
+    "coop0": ["-DBB_STEP_COOP=0"],
+    "coopr2": ["-DBB_STEP_COOP_ROUNDS=2"],
+    "coopkw8": ["-DBB_STEP_COOP_KW=8"],
+    "coopkw16": ["-DBB_STEP_COOP_KW=16"],
+    # exact phase (slow_phase_wave): no early exit; both orders' leaves in full
+    "sexit0": ["-DBB_SLOW_EXIT=0"],
+    "sline0": ["-DBB_SLOW_LINE_ONLY=0"],
+    "slm256": ["-DBB_SLOW_LINE_MIN=256"],
+    "slm512": ["-DBB_SLOW_LINE_MIN=512"],
+    "slm1024": ["-DBB_SLOW_LINE_MIN=1024"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
     "diag3": ["-DBB_ROLL_DIAG=3"],
     # NOT reference semantics (instruction-count attribution only): 1 = in-lane quick test, no wave
