@@ -60,6 +60,7 @@ VARIANTS = {
     "mp1": ["-DBB_MULTI_PASSES=1"],
     "mp2": ["-DBB_MULTI_PASSES=2"],
     "mp4": ["-DBB_MULTI_PASSES=4"],
+    "mp6": ["-DBB_MULTI_PASSES=6"],
     # pass leaf tests without the line clear (pair_quick_nc): measured -1.3%, not shipped
     "passnc": ["-DBB_PASS_NC=1"],
     # board convolutions (csrc/bb_conv.hip): forward weight stages (input channels, ring slots);
