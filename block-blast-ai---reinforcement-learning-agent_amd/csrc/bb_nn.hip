@@ -16,9 +16,7 @@
 //             convolution bias gradient sum(dx).
 // Reductions are two-level without atomics: every block writes fp64 partials
 // (its rows, all its channels), one wave per channel adds them up in a fixed
-// order, so results are deterministic run to run.  Partials are stored
-// channel-major, part[c][q][blk], so that wave reads them as contiguous
-// doubles (block-major, every lane's load touched its own cache line).
+// order, so results are deterministic run to run.
 // Layout NCHW or NHWC (channels_last) contiguous, f32 or bf16 activations, f32
 // parameters and stats.  Loads and stores are 16-byte vectors along the
 // contiguous dimension (HW resp. C times the element size % 16 == 0).
@@ -128,7 +126,7 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// NCHW reduction, block (c, s): channel c, images s, s + S, ... -> part[c][q][s].
+// NCHW reduction, block (c, s): channel c, images s, s + S, ... -> part[s][c][kQ].
 template <typename T, bool BWD>
 __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restrict__ x, const void* __restrict__ dy,
                                                              int N, int C, int HW, const float* __restrict__ pre_bias,
@@ -162,13 +160,13 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
   if (threadIdx.x < kQ) {
     double a = 0.0;
     for (int k2 = 0; k2 < kBnThreads / 64; ++k2) a += red[threadIdx.x][k2];
-    part[((int64_t)c * kQ + threadIdx.x) * gridDim.y + blockIdx.y] = a;
+    part[((int64_t)blockIdx.y * C + c) * kQ + threadIdx.x] = a;
   }
 }
 
 // NHWC reduction: thread t owns the V channels of chunk t % cpr of rows
 // t / cpr, t / cpr + rows_per_iter, ... (cpr = C / V divides kBnThreads, so
-// its channels never change); block b writes part[c][q][b] for every c.
+// its channels never change); block b writes part[b][c][kQ] for every c.
 template <typename T, bool BWD>
 __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restrict__ x, const void* __restrict__ dy,
                                                              int R, int C, const float* __restrict__ pre_bias,
@@ -218,7 +216,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
     double a[kQ] = {0.0, 0.0, 0.0};
     for (int rr = 0; rr < rows_per_iter; ++rr)
       for (int m = 0; m < kQ; ++m) a[m] += red[m][(rr * cpr + cc) * V + jc];
-    for (int m = 0; m < kQ; ++m) part[((int64_t)c * kQ + m) * gridDim.x + blockIdx.x] = a[m];
+    for (int m = 0; m < kQ; ++m) part[((int64_t)blockIdx.x * C + c) * kQ + m] = a[m];
   }
 }
 
@@ -228,16 +226,15 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
 //   backward {pre_bias, mean, invstd * weight, bias, invstd, mean(g), mean(g * xhat), -}
 constexpr int kCoef = 8;
 
-// The per-channel sums over the nb block partials part[c][q][blk], one wave
+// The per-channel sums over the nb block partials part[blk][c][kQ], one wave
 // per channel (fixed order), valid in lane 0.
 __device__ __forceinline__ bool channel_sums(const double* __restrict__ part, int nb, int C, int& c, double a[kQ]) {
   c = blockIdx.x * (kBnThreads / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (c >= C) return false;
   a[0] = a[1] = a[2] = 0.0;
-  const double* pc = part + (int64_t)c * kQ * nb;
   for (int blk = lane; blk < nb; blk += 64)
-    for (int m = 0; m < kQ; ++m) a[m] += pc[(int64_t)m * nb + blk];
+    for (int m = 0; m < kQ; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
   for (int m = 0; m < kQ; ++m) a[m] = wave_sum(a[m]);
   return lane == 0;
 }
@@ -429,7 +426,7 @@ void launch_reduce(const Plan& p, int nhwc, const void* x, const void* dy, int N
 }
 
 // Workspace (16-byte aligned): coefficients [C][kCoef] floats (float4 loads),
-// then the block partials [C][kQ][nb] doubles.
+// then the block partials [nb][C][kQ] doubles.
 struct Ws {
   float* coef;
   double* part;
