@@ -105,7 +105,7 @@ def main() -> None:
     ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
                     help="rollout: bb_rollout, T fused env-steps per launch (default); step: one bb_step per env-step")
     ap.add_argument("--shards", type=int, default=1,
-                    help="rollout mode: split the envs into this many handles, one HIP stream each")
+                    help="split the envs into this many handles, one HIP stream each")
     ap.add_argument("--rollout-len", type=int, default=128,
                     help="T, env-steps per bb_rollout launch (default 128 = the reference's PPO horizon n_steps)")
     args = ap.parse_args()
@@ -135,7 +135,7 @@ def main() -> None:
 
     n = args.envs
     offset = rank * n
-    S = max(1, args.shards) if args.mode == "rollout" else 1
+    S = max(1, args.shards)
     assert n % S == 0
     ns = n // S
     T = max(1, args.rollout_len)
@@ -156,29 +156,28 @@ def main() -> None:
                     torch.zeros((T, ns), dtype=torch.int32, device=dev),
                     torch.zeros((T, ns, 3), dtype=torch.int64, device=dev))
         shards.append((e, torch.cuda.Stream(dev) if S > 1 else torch.cuda.current_stream(dev), a, outs))
-    env, _, act, _ = shards[0]
     step_idx = [0]
 
     def one_step(k=1):
         """k bench steps: k bb_step launches (step mode) or k bb_rollout launches of T env-steps each."""
         t = step_idx[0]
-        if args.mode == "step":
-            for j in range(k):
-                env.step(act[(t + j) & 1], next_action=act[(t + j + 1) & 1], policy_seed=POLICY_SEED,
-                         policy_step=t + j + 1)
-            step_idx[0] = t + k
-            return
         cur = torch.cuda.current_stream(dev)
-        for _, st, _, _ in shards:
-            st.wait_stream(cur)
+        if S > 1:
+            for _, st, _, _ in shards:
+                st.wait_stream(cur)
         for j in range(k):  # the action double-buffer flips once per launch
-            for e, st, a, (o_rew, o_term, o_lines, o_act, o_mask) in shards:
+            for e, st, a, outs in shards:
                 with torch.cuda.stream(st):
-                    e.rollout(T, a[0], o_rew, o_term, lines=o_lines, actions_out=o_act, mask_out=o_mask,
-                              next_action=a[1], policy_seed=POLICY_SEED, policy_step0=t + j * T)
+                    if args.mode == "step":
+                        e.step(a[0], next_action=a[1], policy_seed=POLICY_SEED, policy_step=t + j + 1)
+                    else:
+                        o_rew, o_term, o_lines, o_act, o_mask = outs
+                        e.rollout(T, a[0], o_rew, o_term, lines=o_lines, actions_out=o_act, mask_out=o_mask,
+                                  next_action=a[1], policy_seed=POLICY_SEED, policy_step0=t + j * T)
                 a.reverse()
-        for _, st, _, _ in shards:
-            cur.wait_stream(st)
+        if S > 1:
+            for _, st, _, _ in shards:
+                cur.wait_stream(st)
         step_idx[0] = t + k * (1 if args.mode == "step" else T)
 
     one_step(args.warmup)

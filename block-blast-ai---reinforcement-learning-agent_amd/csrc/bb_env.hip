@@ -108,6 +108,13 @@ __device__ __forceinline__ uint32_t lower_half_bcast(uint32_t x) {
   return __builtin_amdgcn_permlane32_swap(x, x, false, false)[0];
 }
 
+// Every lane gets the value of copy 0 of its env (lane l mod kE).
+template <int kE>
+__device__ __forceinline__ uint32_t copy0_bcast(uint32_t x) {
+  if constexpr (kE == 32) return lower_half_bcast(x);
+  else return (uint32_t)__shfl((int)x, (int)(threadIdx.x & 63) % kE);
+}
+
 __device__ __forceinline__ void masks_of(const Tables& t, uint64_t B, uint32_t hand, uint64_t m[3]) {
   const uint32_t used = hand_used(hand);
 #pragma unroll
@@ -647,7 +654,14 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
 #endif
 constexpr int kRollEnvs = BB_ROLL_ENVS;  // 32 (two copies per env), 16 (four) or 64 (one: 1 wave per SIMD)
 static_assert(kRollEnvs == 16 || kRollEnvs == 32 || kRollEnvs == 64, "envs per wave");
-constexpr uint64_t kRollEnvMask = kRollEnvs >= 64 ? ~0ull : ((1ull << (kRollEnvs & 63)) - 1ull);
+#ifndef BB_STEP_ENVS
+#define BB_STEP_ENVS 32  // bb_step's single-step instantiation: envs per wave (64 / copies)
+#endif
+constexpr int kStepEnvs = BB_STEP_ENVS;
+#ifndef BB_STEP_ROLL_BLOCK
+#define BB_STEP_ROLL_BLOCK 512  // bb_step's single-step instantiation: threads per workgroup
+#endif
+constexpr int kStepRollBlock = BB_STEP_ROLL_BLOCK;
 #ifndef BB_ROLL_BLOCK
 #define BB_ROLL_BLOCK 512  // 8 waves: at 65,536 envs one workgroup per CU, both waves of a SIMD in it
 #endif
@@ -692,23 +706,40 @@ constexpr int kRollBlock = BB_ROLL_BLOCK;
 #ifndef BB_ROLL_KSTEP
 #define BB_ROLL_KSTEP BB_ROLL_SLOTS  // copy c tests slots c * KSTEP, c * KSTEP + 1, ...
 #endif
+#ifndef BB_WG_BALANCE
+// hand searches balanced over the workgroup: after the in-lane quick tests every wave publishes its parked
+// envs to LDS and each of the 8 waves searches an equal share of the workgroup's parked envs (two barriers
+// per step).  1: bb_step's single step only; 2: also every step of bb_rollout; 0: off (each wave searches
+// its own parked envs).  Measured slower and off: bb_step 2.71e9 vs 2.83e9 env-steps/s (the slowest wave is
+// set by its hardest env, not by how many it holds), bb_rollout 5.65e9 vs 8.96e9 (profiles/r03/wgb/)
+#define BB_WG_BALANCE 0
+#endif
+
+// One parked env handed to another wave of the workgroup (BB_WG_BALANCE): the board and stream state on
+// the way in; the stream state and hand ids on the way back.
+struct ParkRec {
+  uint64_t B, hi, lo, inc_hi, inc_lo;
+  uint32_t buf, has, ids, pad;
+};
 
 // kStepOut: the bb_step outputs (info record, fp64 reward) are written too --
 // the instantiation bb_step uses at T = 1; the rollout path runs without them.
 // kSingle: one step per launch (bb_step): the seeded-reset state is read and
 // expanded only by the envs that terminate, and only the state columns the
 // step changed are written back.
-template <bool kStepOut, bool kSingle>
-__global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
+template <bool kStepOut, bool kSingle, int kE, int kBlock>
+__global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e, const PieceRow* g_rows, const uint8_t* g_d,
                                                              StepArgs a, RollArgs r) {
+  static_assert(kE == 8 || kE == 16 || kE == 32 || kE == 64, "envs per wave");
+  constexpr uint64_t kEnvMask = kE >= 64 ? ~0ull : ((1ull << (kE & 63)) - 1ull);
   __shared__ Tables t;
-  __shared__ uint32_t scratch[kRollBlock];  // 64 words per wave (slow_phase_wave)
+  __shared__ uint32_t scratch[kBlock];  // 64 words per wave (slow_phase_wave)
   uint32_t* lds = scratch + (threadIdx.x & ~63);
   __shared__ JumpRow jt[kJumpMax + 1];
   const int lane = threadIdx.x & 63;
-  const int half = lane / kRollEnvs;  // copy index; 0 = primary copy of the env (stores)
-  const int wave = (blockIdx.x * kRollBlock + threadIdx.x) >> 6;
-  const int i = wave * kRollEnvs + (lane % kRollEnvs);
+  const int half = lane / kE;  // copy index; 0 = primary copy of the env (stores)
+  const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int i = wave * kE + (lane % kE);
   const bool live = i < e.n;
   const bool primary = live && half == 0;
   // bb_step (kSingle, T = 1): the seeded-reset state (seed words, has_seed) is read only by the envs
@@ -751,7 +782,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   // nearly unimpeded and the younger one finishes up to 1.3x later, which
   // sets the launch time.  Partners (same workgroup, same SIMD) publish their
   // step counters in LDS; the one behind takes the higher priority.
-  constexpr int kWaves = kRollBlock / 64;
+  constexpr int kWaves = kBlock / 64;
   __shared__ uint32_t wave_simd[kWaves];
   __shared__ uint32_t prog[kWaves];
   const int wv = threadIdx.x >> 6;
@@ -765,7 +796,11 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   for (int k = 0; k < kWaves; ++k)
     if (k != wv && wave_simd[k] == wave_simd[wv]) pw = k;
   const uint32_t tie = wv < pw ? 1u : 0u;
-  if (__ballot(live) == 0ull) return;  // wave-uniform
+  // the balanced search synchronises the workgroup every step: a wave without envs still joins the barriers
+  constexpr bool kBalance = kSingle ? (BB_WG_BALANCE >= 1) : (BB_WG_BALANCE >= 2);
+  __shared__ ParkRec prec[kBalance ? kWaves * kE : 1];
+  __shared__ uint32_t pcnt[kWaves];
+  if (!kBalance && __ballot(live) == 0ull) return;  // wave-uniform
   if (live) s.rng.has = hand_has32(s.hand);
   // A seeded env re-seeds with seed_value on every reset (block_blast_env.py:212-215), so its
   // post-reset hand, stream and mask are the same each episode: computed once, kept in registers.
@@ -796,7 +831,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
   // The policy uniforms are shared by an env's copies: on every kCopies-th
   // step copy c draws the uniform of step + 1 + c, and each step reads its
   // uniform from the copy that drew it (one Philox per lane per kCopies steps).
-  constexpr int kCopies = 64 / kRollEnvs;
+  constexpr int kCopies = 64 / kE;
   uint32_t u_drawn = 0;
 #pragma unroll 1
   for (int step = 0; step < r.steps; ++step) {
@@ -818,7 +853,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
     // same counter again on odd steps
     u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i,
                              r.policy_step0 + (uint64_t)(step - step % kCopies) + 1 + half);
-    const uint32_t u_next = __shfl(u_drawn, (lane % kRollEnvs) + kRollEnvs * (step % kCopies));
+    const uint32_t u_next = __shfl(u_drawn, (lane % kE) + kE * (step % kCopies));
 #endif
     BB_DIAG_T(c0);
     bool park = false;
@@ -859,8 +894,8 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
         s.hand = ids0;
       }
     }
-    const uint32_t idq = lower_half_bcast((uint32_t)ids0 | ((uint32_t)drew0 << 31));
-    const uint64_t Bq = ((uint64_t)lower_half_bcast((uint32_t)(s.B >> 32)) << 32) | lower_half_bcast((uint32_t)s.B);
+    const uint32_t idq = copy0_bcast<kE>((uint32_t)ids0 | ((uint32_t)drew0 << 31));
+    const uint64_t Bq = ((uint64_t)copy0_bcast<kE>((uint32_t)(s.B >> 32)) << 32) | copy0_bcast<kE>((uint32_t)s.B);
     if (live && (idq >> 31)) {
       park = !quick_slot_bf(Bq, idq & 63u, (idq >> 6) & 63u, (idq >> 12) & 63u, t.row, t.d, half * BB_ROLL_KSTEP);
     }
@@ -903,14 +938,15 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #endif
     // accept if either copy accepted; else roll back for the wave search
 #if BB_ROLL_HALF_IDLE
-    uint64_t drew_bits = __ballot(live && half == 0 && s.drew);  // copy 1 did not move: copy 0's flags
-    drew_bits |= drew_bits << 32;
+    uint64_t drew_bits = __ballot(live && half == 0 && s.drew);  // the other copies did not move: copy 0's flags
+#pragma unroll
+    for (int sft = kE; sft < 64; sft <<= 1) drew_bits |= drew_bits << sft;
     uint64_t acc = ~__ballot(park) & drew_bits;
 #else
     uint64_t acc = ~__ballot(park) & __ballot(live && s.drew);
 #endif
-    if (kRollEnvs < 64) acc |= (acc >> (kRollEnvs & 63)) | (acc << ((64 - kRollEnvs) & 63));  // every copy sees the others
-    if (kRollEnvs == 16) acc |= (acc >> 32) | (acc << 32);
+#pragma unroll
+    for (int sft = kE; sft < 64; sft <<= 1) acc |= (acc >> sft) | (acc << (64 - sft));  // every copy sees the others
     const bool accepted = (acc >> lane) & 1ull;
     if (live && s.drew && (!BB_ROLL_HALF_IDLE || half == 0)) {
       rng_moved = true;
@@ -921,19 +957,92 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
       s.hand = (s.hand & 0x3FFFFu) | ((uint32_t)s.rng.has << 22);
     }
     // hand searches the in-lane test left open: the whole wave, one env at a time
-    uint64_t parked = __ballot(park) & kRollEnvMask;
+    uint64_t parked = __ballot(park) & kEnvMask;
     BB_DIAG_T(c1);
+    if constexpr (kBalance) {
+      // publish this wave's parked envs (record wv * kE + rank), then search slice wv of the
+      // workgroup's list: envs gs .. ge-1 of the parked envs in wave order, held by lanes 0 .. ge-gs-1
+      const int el = lane % kE;
+      if (lane < kE && ((parked >> el) & 1ull)) {
+        ParkRec& R = prec[wv * kE + __popcll(parked & ((1ull << el) - 1ull))];
+        R.B = s.B;
+        R.hi = s.rng.hi;
+        R.lo = s.rng.lo;
+        R.inc_hi = s.rng.inc_hi;
+        R.inc_lo = s.rng.inc_lo;
+        R.buf = s.rng.buf;
+        R.has = s.rng.has;
+      }
+      if (lane == 0) pcnt[wv] = (uint32_t)__popcll(parked);
+      __syncthreads();
+      uint32_t cnt[kWaves];
+      uint32_t P = 0;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) {
+        cnt[q] = pcnt[q];
+        P += cnt[q];
+      }
+      if (P) {  // workgroup-uniform
+        const int gs = (int)((wv * P) / kWaves), m = (int)(((wv + 1) * P) / kWaves) - gs;  // m <= kE
+        int rec = 0;
+        Pcg br = s.rng;
+        uint64_t bB = 0ull;
+        if (el < m) {
+          int g = gs + el, q = 0;
+#pragma unroll
+          for (int w = 0; w < kWaves - 1; ++w)
+            if (q == w && g >= (int)cnt[w]) {
+              g -= (int)cnt[w];
+              q = w + 1;
+            }
+          rec = q * kE + g;
+          const ParkRec& R = prec[rec];
+          bB = R.B;
+          br.hi = R.hi;
+          br.lo = R.lo;
+          br.inc_hi = R.inc_hi;
+          br.inc_lo = R.inc_lo;
+          br.buf = R.buf;
+          br.has = R.has;
+        }
+        if (m) {
+          uint32_t ids = 0;
+          gen_hands_multi<kE, kSingle>((1ull << m) - 1ull, bB, br, ids, t.row, t.d, jt, lane, a.pack_first,
+                                              a.pack_next, lds);
+          if (lane < kE && el < m) {
+            ParkRec& R = prec[rec];
+            R.hi = br.hi;
+            R.lo = br.lo;
+            R.buf = br.buf;
+            R.has = br.has;
+            R.ids = ids;
+          }
+        }
+        __syncthreads();
+        if ((parked >> el) & 1ull) {
+          const ParkRec& R = prec[wv * kE + __popcll(parked & ((1ull << el) - 1ull))];
+          s.rng.hi = R.hi;
+          s.rng.lo = R.lo;
+          s.rng.buf = R.buf;
+          s.rng.has = R.has;
+          s.hand = R.ids | (R.has << 22);
+        }
+      }
+#if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
+      dg[3] += (uint64_t)__popcll(parked);
+#endif
+    } else
 #if BB_MULTI
     if (parked) {
       uint32_t ids = 0;
 #if defined(BB_ROLL_DIAG) && BB_ROLL_DIAG == 3
       dg[3] += (uint64_t)__popcll(parked);
-      gen_hands_multi<kRollEnvs, kSingle>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds,
+      gen_hands_multi<kE, kSingle>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds,
                                  &dg[9]);
 #else
-      gen_hands_multi<kRollEnvs, kSingle>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+      gen_hands_multi<kE, kSingle>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
 #endif
-      if ((parked >> (lane % kRollEnvs)) & 1ull) s.hand = ids | ((uint32_t)s.rng.has << 22);
+      if ((parked >> (lane % kE)) & 1ull) s.hand = ids | ((uint32_t)s.rng.has << 22);
     }
 #else
     while (parked) {
@@ -960,7 +1069,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #else
       gen_hand_wave(wB, w, ids, 0, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
 #endif
-      if ((lane % kRollEnvs) == k) {
+      if ((lane % kE) == k) {
         s.rng = w;
         s.hand = ids | ((uint32_t)w.has << 22);
       }
@@ -970,7 +1079,7 @@ __global__ void __launch_bounds__(kRollBlock, BB_ROLL_MINW) rollout_kernel(EnvDe
 #if !BB_ROLL_PHILOX_TOP
     if (step % kCopies == 0)
       u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + step + 1 + half);
-    const uint32_t u_next = __shfl(u_drawn, (lane % kRollEnvs) + kRollEnvs * (step % kCopies));
+    const uint32_t u_next = __shfl(u_drawn, (lane % kE) + kE * (step % kCopies));
 #endif
     if (live && (!BB_ROLL_HALF_IDLE || half == 0)) {
       masks_of(t, s.B, s.hand, m);
@@ -1223,18 +1332,19 @@ hipError_t launch_step(const EnvDev& e, const PieceRow* rows, const uint8_t* d, 
 
 hipError_t launch_rollout(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const StepArgs& a,
                           const RollArgs& r, hipStream_t s) {
-  const int64_t waves = ((int64_t)e.n + kRollEnvs - 1) / kRollEnvs;
-  const int64_t blocks = (waves * 64 + kRollBlock - 1) / kRollBlock;
-  const dim3 g((unsigned)blocks), b(kRollBlock);
+  auto grid = [&](int epw, int blk) { return dim3((unsigned)((((int64_t)e.n + epw - 1) / epw * 64 + blk - 1) / blk)); };
   if (r.steps == 1) {  // bb_step
+    const dim3 g = grid(kStepEnvs, kStepRollBlock), b(kStepRollBlock);
     if (r.info || r.reward_f64)
-      hipLaunchKernelGGL((rollout_kernel<true, true>), g, b, 0, s, e, rows, d, a, r);
+      hipLaunchKernelGGL((rollout_kernel<true, true, kStepEnvs, kStepRollBlock>), g, b, 0, s, e, rows, d, a, r);
     else
-      hipLaunchKernelGGL((rollout_kernel<false, true>), g, b, 0, s, e, rows, d, a, r);
-  } else if (r.info || r.reward_f64) {
-    hipLaunchKernelGGL((rollout_kernel<true, false>), g, b, 0, s, e, rows, d, a, r);
+      hipLaunchKernelGGL((rollout_kernel<false, true, kStepEnvs, kStepRollBlock>), g, b, 0, s, e, rows, d, a, r);
   } else {
-    hipLaunchKernelGGL((rollout_kernel<false, false>), g, b, 0, s, e, rows, d, a, r);
+    const dim3 g = grid(kRollEnvs, kRollBlock), b(kRollBlock);
+    if (r.info || r.reward_f64)
+      hipLaunchKernelGGL((rollout_kernel<true, false, kRollEnvs, kRollBlock>), g, b, 0, s, e, rows, d, a, r);
+    else
+      hipLaunchKernelGGL((rollout_kernel<false, false, kRollEnvs, kRollBlock>), g, b, 0, s, e, rows, d, a, r);
   }
   return hipGetLastError();
 }

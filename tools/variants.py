@@ -106,6 +106,19 @@ VARIANTS = {
     "slm256": ["-DBB_SLOW_LINE_MIN=256"],
     "slm512": ["-DBB_SLOW_LINE_MIN=512"],
     "slm1024": ["-DBB_SLOW_LINE_MIN=1024"],
+    # hand searches balanced over the workgroup's 8 waves (BB_WG_BALANCE, measured slower, shipped 0):
+    # 1 = bb_step only; 2 = bb_rollout's steps too
+    "wgb1": ["-DBB_WG_BALANCE=1"],
+    "wgb2": ["-DBB_WG_BALANCE=2"],
+    # bb_step's single-step instantiation with 16 / 8 envs per wave (4 / 8 copies, as many quick-test slots;
+    # 4,096 / 8,192 waves at 65,536 envs: more waves than resident slots, so the dispatcher balances them)
+    "st16": ["-DBB_STEP_ENVS=16"],
+    "st8": ["-DBB_STEP_ENVS=8"],
+    # ... and with 256 / 128-thread workgroups (BB_STEP_ROLL_BLOCK; 3 resident waves per SIMD at <= 168 VGPRs)
+    "st32b256": ["-DBB_STEP_ROLL_BLOCK=256"],
+    "st16b256": ["-DBB_STEP_ENVS=16", "-DBB_STEP_ROLL_BLOCK=256"],
+    "st8b256": ["-DBB_STEP_ENVS=8", "-DBB_STEP_ROLL_BLOCK=256"],
+    "st16b128": ["-DBB_STEP_ENVS=16", "-DBB_STEP_ROLL_BLOCK=128"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
     "diag3": ["-DBB_ROLL_DIAG=3"],
     # NOT reference semantics (instruction-count attribution only): 1 = in-lane quick test, no wave
