@@ -1216,6 +1216,347 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 }
 
 // ---------------------------------------------------------------------------
+// bb_rollout with the hand searches taken off the step loop.
+//
+// rollout_kernel runs a wave's parked envs through the wave search inside the
+// step: the whole wave (32 envs) waits for it, and with two waves per SIMD at
+// 65,536 envs both are latency-bound (~41% VALU issue).  Here a workgroup holds
+// kAEW env waves (32 envs each, the same two-copy layout and step code) and
+// kASW search waves.  An env whose new hand the in-lane quick test leaves open
+// posts its post-move board and rolled-back stream to an LDS record and is
+// blocked; its wave goes on stepping its other envs (each env keeps its own
+// step counter, outputs go to [its step][N]).  A search wave polls the records
+// of its env waves, runs gen_hands_multi over every posted env at once and
+// returns stream + hand; the env finalizes that step on its next iteration.
+// Each env's trajectory is the one rollout_kernel computes (the same draws,
+// the same tests, the same Philox keys), so the outputs are identical; only
+// the order in which a wave's envs advance changes.  The SIMD gets a third
+// wave of independent work, and a search no longer stalls 31 other envs.
+//
+// Termination: an env wave ends when each of its envs has done T steps (it
+// never waits: blocked envs are polled once per iteration), and raises its
+// flag; a search wave ends when the flags of all its env waves are up (a wave
+// raises it only after every request it posted was answered).  An iteration
+// cap on the env waves bounds the kernel even if a record were lost.
+// ---------------------------------------------------------------------------
+#ifndef BB_ASYNC
+#define BB_ASYNC 1  // bb_rollout without bb_step outputs: env waves + search waves (0: rollout_kernel)
+#endif
+#ifndef BB_ASYNC_EW
+#define BB_ASYNC_EW 8  // env waves per workgroup (32 envs each)
+#endif
+#ifndef BB_ASYNC_SW
+#define BB_ASYNC_SW 4  // search waves per workgroup; each serves BB_ASYNC_EW / BB_ASYNC_SW env waves (<= 64 envs)
+#endif
+#ifndef BB_ASYNC_SPRIO
+#define BB_ASYNC_SPRIO 1  // s_setprio of the search waves while they search
+#endif
+#ifndef BB_ASYNC_SLEEP
+#define BB_ASYNC_SLEEP 1  // s_sleep of an idle search wave between polls
+#endif
+constexpr int kAEW = BB_ASYNC_EW, kASW = BB_ASYNC_SW;
+constexpr int kAServe = kAEW / kASW;  // env waves per search wave
+static_assert(kAEW % kASW == 0 && (kAServe == 1 || kAServe == 2), "a search wave serves <= 64 envs");
+constexpr int kABlock = 64 * (kAEW + kASW);
+constexpr int kAEnvs = 32 * kAEW;  // envs per workgroup
+
+// One posted env: the board and stream state on the way in; stream state and hand ids on the way back.
+struct ARec {
+  uint64_t B, hi, lo;
+  uint32_t buf, has_ids;  // has | ids << 1 on the way back
+};
+
+__global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, const PieceRow* g_rows,
+                                                                  const uint8_t* g_d, StepArgs a, RollArgs r) {
+  constexpr int kE = 32;
+  __shared__ Tables t;
+  __shared__ uint32_t scratch[kABlock];  // 64 words per wave (the search waves' slow_phase_wave)
+  __shared__ JumpRow jt[kJumpMax + 1];
+  __shared__ ARec arec[kAEnvs];
+  __shared__ uint32_t astat[kAEnvs];  // 0 idle, 1 posted, 2 answered
+  __shared__ uint32_t afin[kAEW];
+  __shared__ uint32_t wave_simd[kAEW + kASW];
+  __shared__ uint32_t prog[kAEW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint32_t* lds = scratch + (threadIdx.x & ~63);
+  if (threadIdx.x < kAEnvs) astat[threadIdx.x] = 0u;
+  if (threadIdx.x < kAEW) afin[threadIdx.x] = 0u;
+  if (lane == 0) {
+    wave_simd[wv] = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;  // HW_ID.SIMD_ID
+    if (wv < kAEW) prog[wv] = 0u;
+  }
+  stage_tables<true>(t, g_rows, g_d, jt, a.jump);  // ends with __syncthreads (also orders the inits above)
+
+  if (wv >= kAEW) {
+    // ---------------- search wave: serves env waves sw * kAServe .. + kAServe - 1 ----------------
+    const int sw = wv - kAEW;
+    const int rid = sw * kAServe * 32 + lane;  // the record this lane watches
+    const bool mine = lane < 32 * kAServe;
+    const int gi = blockIdx.x * kAEnvs + rid;
+    Pcg rng;
+    rng.hi = rng.lo = 0ull;
+    rng.buf = 0u;
+    rng.has = 0u;
+    rng.inc_hi = rng.inc_lo = 0ull;
+    if (mine && gi < e.n) {
+      rng.inc_hi = e.inc_hi[gi];
+      rng.inc_lo = e.inc_lo[gi];
+    }
+    uint64_t B = 0ull;
+#pragma unroll 1
+    for (;;) {
+      const uint32_t sv = mine ? __hip_atomic_load(&astat[rid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+      const uint64_t req = __ballot(sv == 1u);
+      if (req) {
+        wave_lds_fence();
+        if (sv == 1u) {
+          const ARec& R = arec[rid];
+          B = R.B;
+          rng.hi = R.hi;
+          rng.lo = R.lo;
+          rng.buf = R.buf;
+          rng.has = R.has_ids & 1u;
+        }
+        __builtin_amdgcn_s_setprio(BB_ASYNC_SPRIO);
+        uint32_t ids = 0;
+        gen_hands_multi<64, false>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+        __builtin_amdgcn_s_setprio(0);
+        if (sv == 1u) {
+          ARec& R = arec[rid];
+          R.hi = rng.hi;
+          R.lo = rng.lo;
+          R.buf = rng.buf;
+          R.has_ids = (rng.has ? 1u : 0u) | (ids << 1);
+        }
+        wave_lds_fence();
+        if (sv == 1u) __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        uint32_t fin = 1u;
+#pragma unroll
+        for (int q = 0; q < kAServe; ++q)
+          fin &= __hip_atomic_load(&afin[sw * kAServe + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (fin) break;  // wave-uniform (LDS word read by every lane)
+        __builtin_amdgcn_s_sleep(BB_ASYNC_SLEEP);
+      }
+    }
+    return;
+  }
+
+  // ---------------- env wave ----------------
+  const int half = lane / kE;  // copy index; 0 = primary copy of the env (stores)
+  const int el = lane % kE;
+  const int rid = wv * kE + el;  // this env's record
+  const int i = blockIdx.x * kAEnvs + rid;
+  const bool live = i < e.n;
+  const bool primary = live && half == 0;
+  StepCtx s;
+  s.seed_hi = s.seed_lo = 0ull;
+  s.has_seed = false;
+  int act = 0;
+  uint64_t m[3] = {0ull, 0ull, 0ull};
+  if (live) {
+    s.i = i;
+    act = r.first_action[i];
+    s.B = e.board[i];
+    s.hand = e.hand[i];
+    s.score = e.score[i];
+    s.combo = e.combo[i];
+    s.max_combo = e.max_combo[i];
+    s.moves = e.moves[i];
+    s.lines_tot = e.lines[i];
+    s.blocks = e.blocks[i];
+    s.prev = e.prev[i];
+    s.rng.hi = e.rng_hi[i];
+    s.rng.lo = e.rng_lo[i];
+    s.rng.buf = e.rng_buf[i];
+    s.rng.inc_hi = e.inc_hi[i];
+    s.rng.inc_lo = e.inc_lo[i];
+    s.seed_hi = e.seed_hi[i];
+    s.seed_lo = e.seed_lo[i];
+    s.has_seed = e.has_seed[i] != 0;
+    s.rng.has = hand_has32(s.hand);
+  }
+  int pw = wv;  // partner: the other env wave of this workgroup on this SIMD
+#pragma unroll
+  for (int k = 0; k < kAEW; ++k)
+    if (k != wv && wave_simd[k] == wave_simd[wv]) pw = k;
+  const uint32_t tie = wv < pw ? 1u : 0u;
+  // seeded envs re-seed on every reset (block_blast_env.py:212-215): post-reset hand, stream, mask once
+  Pcg rs = s.rng;
+  uint32_t r_hand = 0;
+  uint64_t rm[3] = {0ull, 0ull, 0ull};
+  if (live && s.has_seed) {
+    uint64_t B0;
+    reset_lane(t, true, s.seed_hi, s.seed_lo, rs, B0, r_hand, rm);
+  }
+  const size_t N = (size_t)e.n;
+  const int T = r.steps;
+  int st = 0;   // this env's completed steps
+  int ph = 0;   // copy 0: 0 ready to move, 1 posted (blocked), 2 hand known (finalize)
+  uint32_t u_drawn = 0;
+  uint32_t partner = 0;
+  const int cap = 4 * T + 4096;  // iterations: T plus the blocked ones; far above any real count
+#pragma unroll 1
+  for (int it = 0; it < cap; ++it) {
+    if (!__ballot(primary && st < T)) break;
+    {  // the wave behind its SIMD partner (LDS iteration counters) takes the priority
+      const int32_t lead = it - (int32_t)partner;
+      if (lead < 0 || (lead == 0 && (((uint32_t)it ^ tie) & 1u))) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+      if (lane == 0) __hip_atomic_store(&prog[wv], (uint32_t)it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      partner = __hip_atomic_load(&prog[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // 1. answered searches: the stream after the accepted attempt and its hand
+    if (primary && ph == 1) {
+      if (__hip_atomic_load(&astat[rid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
+        wave_lds_fence();
+        const ARec& R = arec[rid];
+        s.rng.hi = R.hi;
+        s.rng.lo = R.lo;
+        s.rng.buf = R.buf;
+        const uint32_t hi = R.has_ids;
+        s.rng.has = hi & 1u;
+        s.hand = (hi >> 1) | ((hi & 1u) << 22);
+        astat[rid] = 0u;
+        ph = 2;
+      }
+    }
+    // 2. the move of every ready env; a drawn hand is quick-tested by both copies (copy 1 takes the
+    //    post-move board and the drawn pieces from copy 0, as in rollout_kernel)
+    const bool mv = primary && ph == 0 && st < T;
+    Pcg after = s.rng;
+    uint32_t ids0 = 0;
+    bool drew0 = false;
+    if (mv) {
+      drew0 = apply_move_bf(t, s, act);
+      if (drew0) {
+        const Pcg save = s.rng;
+        uint32_t x0, x1, x2;
+        draw3(s.rng, x0, x1, x2);
+        ids0 = x0 | (x1 << 6) | (x2 << 12);
+        after = s.rng;
+        s.rng = save;
+        s.hand = ids0;
+      }
+    }
+    const uint32_t idq = copy0_bcast<kE>((uint32_t)ids0 | ((uint32_t)drew0 << 31));
+    const uint64_t Bq = ((uint64_t)copy0_bcast<kE>((uint32_t)(s.B >> 32)) << 32) | copy0_bcast<kE>((uint32_t)s.B);
+    bool park = false;
+    if (live && (idq >> 31))
+      park = !quick_slot_bf(Bq, idq & 63u, (idq >> 6) & 63u, (idq >> 12) & 63u, t.row, t.d, half * BB_ROLL_KSTEP);
+    const uint64_t rej = __ballot(park);
+    const bool accepted = !((rej >> el) & 1ull) || !((rej >> (el + kE)) & 1ull);  // either copy accepted
+    if (mv) {
+      if (drew0) {
+        if (accepted) s.rng = after;
+        s.hand = (s.hand & 0x3FFFFu) | ((uint32_t)s.rng.has << 22);
+        if (accepted) {
+          ph = 2;
+        } else {  // post the env: post-move board, stream rolled back to attempt 1
+          ARec& R = arec[rid];
+          R.B = s.B;
+          R.hi = s.rng.hi;
+          R.lo = s.rng.lo;
+          R.buf = s.rng.buf;
+          R.has_ids = s.rng.has ? 1u : 0u;
+          wave_lds_fence();
+          __hip_atomic_store(&astat[rid], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          ph = 1;
+        }
+      } else {
+        ph = 2;  // no draw (or an invalid action): the hand is known
+      }
+    }
+    // 3. the policy uniforms: copy c draws the uniform of step st + 1 + c on the env's even steps
+    const bool fin = primary && ph == 2;
+    const uint32_t sb = copy0_bcast<kE>((uint32_t)st | ((uint32_t)fin << 31));
+    const int stc = (int)(sb & 0x7FFFFFFFu);
+    if ((sb >> 31) && (stc & 1) == 0)
+      u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + stc + 1 + half);
+    const uint32_t u_next = __shfl(u_drawn, el + kE * (stc & 1));
+    // 4. finalize every env whose hand is known (rollout_kernel's finalize)
+    if (fin) {
+      masks_of(t, s.B, s.hand, m);
+      double rew = -10.0;  // invalid action (block_blast_env.py:240-245)
+      bool term = false;
+      int holes = 0;
+      if (s.valid) {
+        const bool over = (m[0] | m[1] | m[2]) == 0ull;  // engine.py:440-441
+        if (over) s.hand |= 1u << 21;
+        int center;
+        rew = move_reward(s, a, over, holes, center);
+        s.prev = (uint32_t)(holes | (center << 8));
+        term = over;
+      }
+      const size_t o = (size_t)st * N + (size_t)i;
+      r.reward[o] = (float)rew;
+      r.terminated[o] = term ? 1 : 0;
+      if (r.lines) r.lines[o] = (uint8_t)s.lines;
+      if (r.actions) r.actions[o] = act;
+      if (term) {  // info['final_score'] / info['moves'] of the ending episode (wrappers.py:97-101)
+        if (r.final_score) r.final_score[o] = s.score;
+        if (r.final_moves) r.final_moves[o] = s.moves;
+      }
+      if (term && a.autoreset) {  // wrappers.py:97-102
+        if (s.has_seed) {
+          s.B = 0ull;
+          s.hand = r_hand;
+          s.rng.hi = rs.hi;
+          s.rng.lo = rs.lo;
+          s.rng.buf = rs.buf;
+          s.rng.has = rs.has;
+          m[0] = rm[0];
+          m[1] = rm[1];
+          m[2] = rm[2];
+        } else {  // seed_value None: the stream continues across episodes
+          reset_lane(t, false, s.seed_hi, s.seed_lo, s.rng, s.B, s.hand, m);
+        }
+        s.score = 0;
+        s.combo = 0;
+        s.max_combo = 0;
+        s.moves = 0;
+        s.lines_tot = 0;
+        s.blocks = 0;
+        s.prev = 0;
+      }
+      if (r.mask) {
+        r.mask[3 * o + 0] = m[0];
+        r.mask[3 * o + 1] = m[1];
+        r.mask[3 * o + 2] = m[2];
+      }
+      act = random_policy_u(m[0], m[1], m[2], u_next);  // Philox (seed, env, policy_step0 + step + 1)
+      st += 1;
+      ph = 0;
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  if (primary) {
+    e.board[i] = s.B;
+    e.hand[i] = s.hand;
+    e.rng_hi[i] = s.rng.hi;
+    e.rng_lo[i] = s.rng.lo;
+    e.rng_buf[i] = s.rng.buf;
+    e.score[i] = s.score;
+    e.combo[i] = s.combo;
+    e.max_combo[i] = s.max_combo;
+    e.moves[i] = s.moves;
+    e.lines[i] = s.lines_tot;
+    e.blocks[i] = s.blocks;
+    e.prev[i] = (uint16_t)s.prev;
+    if (T > 0) {
+      e.mask[3 * i + 0] = m[0];
+      e.mask[3 * i + 1] = m[1];
+      e.mask[3 * i + 2] = m[2];
+    }
+    if (r.next_action) r.next_action[i] = act;
+  }
+  // every request this wave posted has been answered (an env is posted only while st < T)
+  wave_lds_fence();
+  if (lane == 0) __hip_atomic_store(&afin[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ---------------------------------------------------------------------------
 // Observation expansion: engine.py:478-507 / block_blast_env.py:134-146.
 // One thread per 16-byte output chunk -> fully coalesced dwordx4 stores.
 // ---------------------------------------------------------------------------
@@ -1339,6 +1680,9 @@ hipError_t launch_rollout(const EnvDev& e, const PieceRow* rows, const uint8_t* 
       hipLaunchKernelGGL((rollout_kernel<true, true, kStepEnvs, kStepRollBlock>), g, b, 0, s, e, rows, d, a, r);
     else
       hipLaunchKernelGGL((rollout_kernel<false, true, kStepEnvs, kStepRollBlock>), g, b, 0, s, e, rows, d, a, r);
+  } else if (BB_ASYNC && kRollEnvs == 32 && !r.info && !r.reward_f64) {
+    const dim3 g((unsigned)(((int64_t)e.n + kAEnvs - 1) / kAEnvs)), b(kABlock);
+    hipLaunchKernelGGL(rollout_async_kernel, g, b, 0, s, e, rows, d, a, r);
   } else {
     const dim3 g = grid(kRollEnvs, kRollBlock), b(kRollBlock);
     if (r.info || r.reward_f64)

@@ -21,6 +21,16 @@ from runtime.build import HIPCC_FLAGS, SOURCES  # noqa: E402  the shipped source
 VARIANTS = {
     # name: extra -D flags on top of the shipped build (runtime/build.py)
     "main": [],
+    # bb_rollout with search waves (rollout_async_kernel) vs in-step wave searches (rollout_kernel)
+    "sync": ["-DBB_ASYNC=0"],
+    "asw8": ["-DBB_ASYNC_SW=8"],
+    "asp0": ["-DBB_ASYNC_SPRIO=0"],
+    "asp2": ["-DBB_ASYNC_SPRIO=2"],
+    "asl4": ["-DBB_ASYNC_SLEEP=4"],
+    "asp3": ["-DBB_ASYNC_SPRIO=3"],
+    "a2sw8": ["-DBB_ASYNC_SPRIO=2", "-DBB_ASYNC_SW=8"],
+    "a2sl0": ["-DBB_ASYNC_SPRIO=2", "-DBB_ASYNC_SLEEP=0"],
+    "a3sw8": ["-DBB_ASYNC_SPRIO=3", "-DBB_ASYNC_SW=8"],
     # rollout kernel workgroup shape (waves per workgroup; SIMD partners share LDS progress words at 512)
     "rblk64": ["-DBB_ROLL_BLOCK=64"],
     "rblk256": ["-DBB_ROLL_BLOCK=256"],
