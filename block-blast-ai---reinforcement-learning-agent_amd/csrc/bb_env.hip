@@ -1249,14 +1249,27 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 #define BB_ASYNC_SW 4  // search waves per workgroup; each serves BB_ASYNC_EW / BB_ASYNC_SW env waves (<= 64 envs)
 #endif
 #ifndef BB_ASYNC_SPRIO
-#define BB_ASYNC_SPRIO 1  // s_setprio of the search waves while they search
+#define BB_ASYNC_SPRIO 3  // s_setprio of the search waves while they search (0: 5.6e9, 1: 9.58e9, 3: 9.60e9)
+#endif
+#ifndef BB_ASYNC_POOL
+#define BB_ASYNC_POOL 1  // every search wave takes posted envs of the whole workgroup (LDS compare-and-swap);
+                         // 0: search wave s serves env waves 2s, 2s+1 (9.60e9 vs 9.89e9 pooled)
+#endif
+#ifndef BB_ASYNC_FAIR
+#define BB_ASYNC_FAIR 1  // env waves: the one behind its SIMD partner takes s_setprio 1 (0: no priority)
+#endif
+#ifndef BB_ASYNC_SLOTS
+#define BB_ASYNC_SLOTS 1  // in-lane quick-test slots per copy (copy c tests slots c * n .. c * n + n - 1)
+#endif
+#ifndef BB_ASYNC_DIAG
+#define BB_ASYNC_DIAG 0  // per-wave counters into dbg_out (tools/diag_async.py, BB_DEBUG_MODE=16)
 #endif
 #ifndef BB_ASYNC_SLEEP
 #define BB_ASYNC_SLEEP 1  // s_sleep of an idle search wave between polls
 #endif
 constexpr int kAEW = BB_ASYNC_EW, kASW = BB_ASYNC_SW;
 constexpr int kAServe = kAEW / kASW;  // env waves per search wave
-static_assert(kAEW % kASW == 0 && (kAServe == 1 || kAServe == 2), "a search wave serves <= 64 envs");
+static_assert(BB_ASYNC_POOL || (kAEW % kASW == 0 && (kAServe == 1 || kAServe == 2)), "a search wave serves <= 64 envs");
 constexpr int kABlock = 64 * (kAEW + kASW);
 constexpr int kAEnvs = 32 * kAEW;  // envs per workgroup
 
@@ -1264,6 +1277,7 @@ constexpr int kAEnvs = 32 * kAEW;  // envs per workgroup
 struct ARec {
   uint64_t B, hi, lo;
   uint32_t buf, has_ids;  // has | ids << 1 on the way back
+  uint64_t inc_hi, inc_lo;  // BB_ASYNC_POOL: the stream increment (any search wave may take the env)
 };
 
 __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, const PieceRow* g_rows,
@@ -1291,22 +1305,48 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
   if (wv >= kAEW) {
     // ---------------- search wave: serves env waves sw * kAServe .. + kAServe - 1 ----------------
     const int sw = wv - kAEW;
-    const int rid = sw * kAServe * 32 + lane;  // the record this lane watches
-    const bool mine = lane < 32 * kAServe;
-    const int gi = blockIdx.x * kAEnvs + rid;
     Pcg rng;
     rng.hi = rng.lo = 0ull;
     rng.buf = 0u;
     rng.has = 0u;
     rng.inc_hi = rng.inc_lo = 0ull;
+#if BB_ASYNC_POOL
+    constexpr int kPer = kAEnvs / 64;  // records watched per lane: k * 64 + lane
+    static_assert(kAEnvs % 64 == 0, "pool: whole records per lane");
+    int rid = lane;
+#else
+    const int rid = sw * kAServe * 32 + lane;  // the record this lane watches
+    const bool mine = lane < 32 * kAServe;
+    const int gi = blockIdx.x * kAEnvs + rid;
     if (mine && gi < e.n) {
       rng.inc_hi = e.inc_hi[gi];
       rng.inc_lo = e.inc_lo[gi];
     }
+#endif
     uint64_t B = 0ull;
+#if BB_ASYNC_DIAG  // diagnostics (BB_DEBUG_MODE=16): calls, envs served, search cycles, polls
+    uint64_t dcalls = 0, denvs = 0, dcyc = 0, dpolls = 0;
+#endif
 #pragma unroll 1
     for (;;) {
+#if BB_ASYNC_POOL
+      // claim the first posted record among this lane's (posted -> 3 by compare-and-swap)
+      uint32_t sv = 0u;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        if (sv != 1u &&
+            __hip_atomic_load(&astat[k * 64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u) {
+          uint32_t expect = 1u;
+          if (__hip_atomic_compare_exchange_strong(&astat[k * 64 + lane], &expect, 3u, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            sv = 1u;
+            rid = k * 64 + lane;
+          }
+        }
+      }
+#else
       const uint32_t sv = mine ? __hip_atomic_load(&astat[rid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+#endif
       const uint64_t req = __ballot(sv == 1u);
       if (req) {
         wave_lds_fence();
@@ -1317,10 +1357,22 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
           rng.lo = R.lo;
           rng.buf = R.buf;
           rng.has = R.has_ids & 1u;
+#if BB_ASYNC_POOL
+          rng.inc_hi = R.inc_hi;
+          rng.inc_lo = R.inc_lo;
+#endif
         }
         __builtin_amdgcn_s_setprio(BB_ASYNC_SPRIO);
         uint32_t ids = 0;
+#if BB_ASYNC_DIAG
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
         gen_hands_multi<64, false>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+#if BB_ASYNC_DIAG
+        dcyc += __builtin_amdgcn_s_memtime() - c0;
+        dcalls += 1;
+        denvs += (uint64_t)__popcll(req);
+#endif
         __builtin_amdgcn_s_setprio(0);
         if (sv == 1u) {
           ARec& R = arec[rid];
@@ -1333,13 +1385,27 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         if (sv == 1u) __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
         uint32_t fin = 1u;
+        constexpr int kWatch = BB_ASYNC_POOL ? kAEW : kAServe;  // env waves whose end this wave waits for
 #pragma unroll
-        for (int q = 0; q < kAServe; ++q)
-          fin &= __hip_atomic_load(&afin[sw * kAServe + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int q = 0; q < kWatch; ++q)
+          fin &= __hip_atomic_load(&afin[BB_ASYNC_POOL ? q : sw * kAServe + q], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
         if (fin) break;  // wave-uniform (LDS word read by every lane)
+#if BB_ASYNC_DIAG
+        dpolls += 1;
+#endif
         __builtin_amdgcn_s_sleep(BB_ASYNC_SLEEP);
       }
     }
+#if BB_ASYNC_DIAG
+    if (a.dbg_out && lane == 0) {
+      uint64_t* o = a.dbg_out + 4 * ((size_t)(e.n + 31) / 32 + (size_t)blockIdx.x * kASW + sw);
+      o[0] = dcalls;
+      o[1] = denvs;
+      o[2] = dcyc;
+      o[3] = dpolls;
+    }
+#endif
     return;
   }
 
@@ -1397,10 +1463,19 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
   uint32_t u_drawn = 0;
   uint32_t partner = 0;
   const int cap = 4 * T + 4096;  // iterations: T plus the blocked ones; far above any real count
+#if BB_ASYNC_DIAG  // iterations, cycles, blocked env-iterations, iterations that moved no env
+  uint64_t dit = 0, dblk = 0, didle = 0;
+  const uint64_t dt0 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll 1
   for (int it = 0; it < cap; ++it) {
     if (!__ballot(primary && st < T)) break;
-    {  // the wave behind its SIMD partner (LDS iteration counters) takes the priority
+#if BB_ASYNC_DIAG
+    dit += 1;
+    dblk += (uint64_t)__popcll(__ballot(primary && ph == 1));
+    didle += __ballot(primary && ph != 1 && st < T) ? 0u : 1u;
+#endif
+    if (BB_ASYNC_FAIR) {  // the wave behind its SIMD partner (LDS iteration counters) takes the priority
       const int32_t lead = it - (int32_t)partner;
       if (lead < 0 || (lead == 0 && (((uint32_t)it ^ tie) & 1u))) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
@@ -1443,8 +1518,13 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     const uint32_t idq = copy0_bcast<kE>((uint32_t)ids0 | ((uint32_t)drew0 << 31));
     const uint64_t Bq = ((uint64_t)copy0_bcast<kE>((uint32_t)(s.B >> 32)) << 32) | copy0_bcast<kE>((uint32_t)s.B);
     bool park = false;
-    if (live && (idq >> 31))
-      park = !quick_slot_bf(Bq, idq & 63u, (idq >> 6) & 63u, (idq >> 12) & 63u, t.row, t.d, half * BB_ROLL_KSTEP);
+    if (live && (idq >> 31)) {
+      const uint32_t q0 = idq & 63u, q1 = (idq >> 6) & 63u, q2 = (idq >> 12) & 63u;
+      bool ok = quick_slot_bf(Bq, q0, q1, q2, t.row, t.d, half * BB_ASYNC_SLOTS);
+#pragma unroll
+      for (int k = 1; k < BB_ASYNC_SLOTS; ++k) ok = ok || quick_slot_bf(Bq, q0, q1, q2, t.row, t.d, half * BB_ASYNC_SLOTS + k);
+      park = !ok;
+    }
     const uint64_t rej = __ballot(park);
     const bool accepted = !((rej >> el) & 1ull) || !((rej >> (el + kE)) & 1ull);  // either copy accepted
     if (mv) {
@@ -1460,6 +1540,10 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
           R.lo = s.rng.lo;
           R.buf = s.rng.buf;
           R.has_ids = s.rng.has ? 1u : 0u;
+          if (BB_ASYNC_POOL) {
+            R.inc_hi = s.rng.inc_hi;
+            R.inc_lo = s.rng.inc_lo;
+          }
           wave_lds_fence();
           __hip_atomic_store(&astat[rid], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           ph = 1;
@@ -1531,6 +1615,15 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     }
   }
   __builtin_amdgcn_s_setprio(0);
+#if BB_ASYNC_DIAG
+  if (a.dbg_out && lane == 0) {
+    uint64_t* o = a.dbg_out + 4 * ((size_t)blockIdx.x * kAEW + wv);
+    o[0] = dit;
+    o[1] = __builtin_amdgcn_s_memtime() - dt0;
+    o[2] = dblk;
+    o[3] = didle;
+  }
+#endif
   if (primary) {
     e.board[i] = s.B;
     e.hand[i] = s.hand;

@@ -163,3 +163,10 @@ def test_rollout_matches_oracle(cuda):
     assert np.array_equal(st["board"], ps["board"])
     for key in ("score", "moves", "lines", "combo", "max_combo", "blocks"):
         assert np.array_equal(st[key].astype(np.int64), ps[key].astype(np.int64)), key
+
+
+def test_rollout_long_horizon(cuda):
+    """A long launch: the envs of a wave drift many steps apart while their hand searches are answered by
+    the search waves (rollout_async_kernel), and every output still lands at its own [step][env]."""
+    n, steps = 2048, 400
+    _assert_same(_chained_steps(n, 0, steps, cuda), _rollout(n, 0, steps, cuda))

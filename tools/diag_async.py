@@ -1,0 +1,70 @@
+"""Diagnostics (not product): per-wave counters of rollout_async_kernel.
+
+Needs a build with -DBB_ASYNC_DIAG=1 (python tools/variants.py build adiag, loaded with
+BBVEC_LIB=tools/variants/libbbvec_adiag.so); sets BB_DEBUG_MODE=16.  Reports per env wave:
+iterations per step (T plus blocked iterations), cycles per iteration, blocked env-iterations
+and iterations that moved no env; per search wave: calls, envs per call, cycles per call, polls.
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+os.environ["BB_DEBUG_MODE"] = "16"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "block-blast-ai---reinforcement-learning-agent_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from runtime.device_env import DeviceEnvBatch  # noqa: E402
+
+
+def main():
+    n = int(os.environ.get("N", "65536"))
+    T = int(os.environ.get("T", "128"))
+    ew, sw = int(os.environ.get("EW", "8")), int(os.environ.get("SW", "4"))
+    dev = torch.device("cuda", 0)
+    env = DeviceEnvBatch(n, seeds=[42 + i for i in range(n)], device=dev)
+    env.reset()
+    mb = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+    env.obs(mask_bits=mb)
+    act = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(2)]
+    env.random_actions(mb, act[0], step=0)
+    rew = torch.zeros((T, n), dtype=torch.float32, device=dev)
+    term = torch.zeros((T, n), dtype=torch.uint8, device=dev)
+    buf = np.zeros((n, 4), dtype=np.uint64)
+    out = []
+    nwe = (n + 31) // 32
+    nws = (n + 32 * ew - 1) // (32 * ew) * sw
+    for call in range(4):
+        env.rollout(T, act[0], rew, term, next_action=act[1], policy_step0=call * T)
+        act.reverse()
+        torch.cuda.synchronize()
+        env.lib.bb_debug_counters(env.handle, buf.ctypes.data_as(C.c_void_p))
+        flat = buf.reshape(-1)
+        we = flat[: 4 * nwe].reshape(-1, 4).astype(np.float64)
+        ws = flat[4 * nwe: 4 * (nwe + nws)].reshape(-1, 4).astype(np.float64)
+        out.append({
+            "call": call, "T": T,
+            "env_iters_per_step": round(we[:, 0].mean() / T, 4),
+            "env_iters_max": int(we[:, 0].max()),
+            "env_cyc_per_iter": round(we[:, 1].sum() / we[:, 0].sum(), 1),
+            "env_wave_cyc_mean": round(we[:, 1].mean(), 0),
+            "env_wave_cyc_max": int(we[:, 1].max()),
+            "blocked_envs_per_iter": round(we[:, 2].sum() / we[:, 0].sum(), 3),
+            "idle_iters_per_wave": round(we[:, 3].mean(), 2),
+            "search_calls_per_wave": round(ws[:, 0].mean(), 1),
+            "envs_per_call": round(ws[:, 1].sum() / max(ws[:, 0].sum(), 1), 2),
+            "cyc_per_call": round(ws[:, 2].sum() / max(ws[:, 0].sum(), 1), 0),
+            "search_busy_frac": round(ws[:, 2].sum() / (we[:, 1].mean() * len(ws)), 3),
+            "polls_per_wave": round(ws[:, 3].mean(), 1),
+        })
+        buf[:] = 0
+        env.lib.bb_debug_counters  # counters are overwritten by every launch
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,17 @@ VARIANTS = {
     "a2sw8": ["-DBB_ASYNC_SPRIO=2", "-DBB_ASYNC_SW=8"],
     "a2sl0": ["-DBB_ASYNC_SPRIO=2", "-DBB_ASYNC_SLEEP=0"],
     "a3sw8": ["-DBB_ASYNC_SPRIO=3", "-DBB_ASYNC_SW=8"],
+    "apool": ["-DBB_ASYNC_POOL=1"],
+    "apool0": ["-DBB_ASYNC_POOL=0"],
+    "apsw8": ["-DBB_ASYNC_SW=8"],
+    "apsw2": ["-DBB_ASYNC_SW=2"],
+    "apsw6": ["-DBB_ASYNC_SW=6"],
+    "afair0": ["-DBB_ASYNC_FAIR=0"],
+    "aslot2": ["-DBB_ASYNC_SLOTS=2"],
+    "apool3": ["-DBB_ASYNC_POOL=1", "-DBB_ASYNC_SPRIO=3"],
+    "adiag": ["-DBB_ASYNC_DIAG=1"],
+    "adiagp": ["-DBB_ASYNC_DIAG=1", "-DBB_ASYNC_POOL=1"],
+    "adiag2": ["-DBB_ASYNC_DIAG=1", "-DBB_ASYNC_SPRIO=2"],
     # rollout kernel workgroup shape (waves per workgroup; SIMD partners share LDS progress words at 512)
     "rblk64": ["-DBB_ROLL_BLOCK=64"],
     "rblk256": ["-DBB_ROLL_BLOCK=256"],
@@ -130,11 +141,11 @@ VARIANTS = {
     "st8b256": ["-DBB_STEP_ENVS=8", "-DBB_STEP_ROLL_BLOCK=256"],
     "st16b128": ["-DBB_STEP_ENVS=16", "-DBB_STEP_ROLL_BLOCK=128"],
     # timing diagnostics of the rollout phases (tools/diag_rollout.py, BB_DEBUG_MODE=16)
-    "diag3": ["-DBB_ROLL_DIAG=3"],
+    "diag3": ["-DBB_ROLL_DIAG=3", "-DBB_ASYNC=0"],
     # NOT reference semantics (instruction-count attribution only): 1 = in-lane quick test, no wave
     # search (an unaccepted draw is kept); 2 = first draw kept, no test at all
-    "diag1": ["-DBB_ROLL_DIAG=1"],
-    "diag2": ["-DBB_ROLL_DIAG=2"],
+    "diag1": ["-DBB_ROLL_DIAG=1", "-DBB_ASYNC=0"],
+    "diag2": ["-DBB_ROLL_DIAG=2", "-DBB_ASYNC=0"],
 }
 
 
