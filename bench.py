@@ -250,7 +250,8 @@ def main() -> None:
                 "kernel": (("bb_step = bb::step_kernel + bb::escalate_kernel (BB_STEP_KERNELS=2)"
                             if os.environ.get("BB_STEP_KERNELS") == "2" else
                             "bb_step = one bb::rollout_kernel<true> launch at T = 1") if args.mode == "step" else
-                           f"bb_rollout = bb::rollout_kernel, {T} env-steps of every env per launch"),
+                           f"bb_rollout = bb::rollout_async_kernel (env waves + search waves), {T} env-steps "
+                           f"of every env per launch"),
                 "env_steps_per_launch": n * per_launch,
                 "kernel_avg_ms": round(kern_ms, 5),
                 "algo_bytes_per_launch": algo_bytes,

@@ -1261,6 +1261,9 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 #ifndef BB_ASYNC_SLOTS
 #define BB_ASYNC_SLOTS 1  // in-lane quick-test slots per copy (copy c tests slots c * n .. c * n + n - 1)
 #endif
+#ifndef BB_ASYNC_LATEPOLL
+#define BB_ASYNC_LATEPOLL 1  // env waves poll their posted envs after the moves (0: before them; 1.017e10 vs 9.89e9)
+#endif
 #ifndef BB_ASYNC_DIAG
 #define BB_ASYNC_DIAG 0  // per-wave counters into dbg_out (tools/diag_async.py, BB_DEBUG_MODE=16)
 #endif
@@ -1483,6 +1486,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
       partner = __hip_atomic_load(&prog[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     // 1. answered searches: the stream after the accepted attempt and its hand
+    auto poll = [&]() {
     if (primary && ph == 1) {
       if (__hip_atomic_load(&astat[rid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
         wave_lds_fence();
@@ -1497,6 +1501,8 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         ph = 2;
       }
     }
+    };
+    if (!BB_ASYNC_LATEPOLL) poll();
     // 2. the move of every ready env; a drawn hand is quick-tested by both copies (copy 1 takes the
     //    post-move board and the drawn pieces from copy 0, as in rollout_kernel)
     const bool mv = primary && ph == 0 && st < T;
@@ -1552,6 +1558,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         ph = 2;  // no draw (or an invalid action): the hand is known
       }
     }
+    if (BB_ASYNC_LATEPOLL) poll();  // after the moves: answers that arrived meanwhile finalize this iteration
     // 3. the policy uniforms: copy c draws the uniform of step st + 1 + c on the env's even steps
     const bool fin = primary && ph == 2;
     const uint32_t sb = copy0_bcast<kE>((uint32_t)st | ((uint32_t)fin << 31));

@@ -13,4 +13,4 @@ f=$(find "$R/gpurun_out/${TAG}_kt" -name "*kernel_stats.csv" | head -1); cp "$f"
 cut -d, -f1-8 "$f" | grep "bb::" | cut -c1-60,200-400
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/${TAG}_fetch" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline $ARGS > "$R/gpurun_out/${TAG}_fetch.log" 2>&1 || { tail -20 "$R/gpurun_out/${TAG}_fetch.log"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/${TAG}_write" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline $ARGS > "$R/gpurun_out/${TAG}_write.log" 2>&1 || { tail -20 "$R/gpurun_out/${TAG}_write.log"; exit 1; }
-python "$R/tools/pmc_traffic.py" "$R/gpurun_out/${TAG}_fetch" "$R/gpurun_out/${TAG}_write" --envs 65536 ${PMC_ARGS:---kernels rollout_kernel --steps-per-launch 128} --out "$R/gpurun_out/${TAG}_pmc.json"
+python "$R/tools/pmc_traffic.py" "$R/gpurun_out/${TAG}_fetch" "$R/gpurun_out/${TAG}_write" --envs 65536 ${PMC_ARGS:---kernels rollout_async_kernel --steps-per-launch 128} --out "$R/gpurun_out/${TAG}_pmc.json"

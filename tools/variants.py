@@ -33,6 +33,8 @@ VARIANTS = {
     "a3sw8": ["-DBB_ASYNC_SPRIO=3", "-DBB_ASYNC_SW=8"],
     "apool": ["-DBB_ASYNC_POOL=1"],
     "apool0": ["-DBB_ASYNC_POOL=0"],
+    "alate": ["-DBB_ASYNC_LATEPOLL=1"],
+    "alatediag": ["-DBB_ASYNC_LATEPOLL=1", "-DBB_ASYNC_DIAG=1"],
     "apsw8": ["-DBB_ASYNC_SW=8"],
     "apsw2": ["-DBB_ASYNC_SW=2"],
     "apsw6": ["-DBB_ASYNC_SW=6"],
