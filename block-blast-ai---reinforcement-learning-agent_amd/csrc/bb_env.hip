@@ -111,7 +111,8 @@ __device__ __forceinline__ uint32_t lower_half_bcast(uint32_t x) {
 // Every lane gets the value of copy 0 of its env (lane l mod kE).
 template <int kE>
 __device__ __forceinline__ uint32_t copy0_bcast(uint32_t x) {
-  if constexpr (kE == 32) return lower_half_bcast(x);
+  if constexpr (kE == 64) return x;
+  else if constexpr (kE == 32) return lower_half_bcast(x);
   else return (uint32_t)__shfl((int)x, (int)(threadIdx.x & 63) % kE);
 }
 
@@ -1242,8 +1243,12 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 #ifndef BB_ASYNC
 #define BB_ASYNC 1  // bb_rollout without bb_step outputs: env waves + search waves (0: rollout_kernel)
 #endif
+#ifndef BB_ASYNC_ENVS
+#define BB_ASYNC_ENVS 64  // envs per env wave: 64 (one lane per env; 4 env + 4 search waves per CU: 1.074e10)
+                          // or 32 (two copies per env, 8 env waves per CU: 1.006e10)
+#endif
 #ifndef BB_ASYNC_EW
-#define BB_ASYNC_EW 8  // env waves per workgroup (32 envs each)
+#define BB_ASYNC_EW (256 / BB_ASYNC_ENVS)  // env waves per workgroup (256 envs: one workgroup per CU at 65,536)
 #endif
 #ifndef BB_ASYNC_SW
 #define BB_ASYNC_SW 4  // search waves per workgroup; each serves BB_ASYNC_EW / BB_ASYNC_SW env waves (<= 64 envs)
@@ -1261,6 +1266,9 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 #ifndef BB_ASYNC_SLOTS
 #define BB_ASYNC_SLOTS 1  // in-lane quick-test slots per copy (copy c tests slots c * n .. c * n + n - 1)
 #endif
+#ifndef BB_ASYNC_SLOTS64
+#define BB_ASYNC_SLOTS64 2  // 64-env waves: in-lane quick-test slots per env (0, 1: the two copies' slots)
+#endif
 #ifndef BB_ASYNC_LATEPOLL
 #define BB_ASYNC_LATEPOLL 1  // env waves poll their posted envs after the moves (0: before them; 1.017e10 vs 9.89e9)
 #endif
@@ -1274,7 +1282,9 @@ constexpr int kAEW = BB_ASYNC_EW, kASW = BB_ASYNC_SW;
 constexpr int kAServe = kAEW / kASW;  // env waves per search wave
 static_assert(BB_ASYNC_POOL || (kAEW % kASW == 0 && (kAServe == 1 || kAServe == 2)), "a search wave serves <= 64 envs");
 constexpr int kABlock = 64 * (kAEW + kASW);
-constexpr int kAEnvs = 32 * kAEW;  // envs per workgroup
+constexpr int kAE = BB_ASYNC_ENVS;
+static_assert(kAE == 32 || kAE == 64, "async env waves: 32 or 64 envs");
+constexpr int kAEnvs = kAE * kAEW;  // envs per workgroup
 
 // One posted env: the board and stream state on the way in; stream state and hand ids on the way back.
 struct ARec {
@@ -1285,7 +1295,8 @@ struct ARec {
 
 __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, const PieceRow* g_rows,
                                                                   const uint8_t* g_d, StepArgs a, RollArgs r) {
-  constexpr int kE = 32;
+  constexpr int kE = kAE;
+  constexpr int kCopies = 64 / kE;
   __shared__ Tables t;
   __shared__ uint32_t scratch[kABlock];  // 64 words per wave (the search waves' slow_phase_wave)
   __shared__ JumpRow jt[kJumpMax + 1];
@@ -1526,13 +1537,17 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     bool park = false;
     if (live && (idq >> 31)) {
       const uint32_t q0 = idq & 63u, q1 = (idq >> 6) & 63u, q2 = (idq >> 12) & 63u;
-      bool ok = quick_slot_bf(Bq, q0, q1, q2, t.row, t.d, half * BB_ASYNC_SLOTS);
+      constexpr int kSl = kE == 64 ? BB_ASYNC_SLOTS64 : BB_ASYNC_SLOTS;  // slots tested by this lane
+      bool ok = quick_slot_bf(Bq, q0, q1, q2, t.row, t.d, half * kSl);
 #pragma unroll
-      for (int k = 1; k < BB_ASYNC_SLOTS; ++k) ok = ok || quick_slot_bf(Bq, q0, q1, q2, t.row, t.d, half * BB_ASYNC_SLOTS + k);
+      for (int k = 1; k < kSl; ++k) ok = quick_slot_bf(Bq, q0, q1, q2, t.row, t.d, half * kSl + k) || ok;
       park = !ok;
     }
     const uint64_t rej = __ballot(park);
-    const bool accepted = !((rej >> el) & 1ull) || !((rej >> (el + kE)) & 1ull);  // either copy accepted
+    uint64_t okb = ~rej;  // either copy accepted
+#pragma unroll
+    for (int sft = kE; sft < 64; sft <<= 1) okb |= (okb >> sft) | (okb << (64 - sft));
+    const bool accepted = (okb >> lane) & 1ull;
     if (mv) {
       if (drew0) {
         if (accepted) s.rng = after;
@@ -1563,9 +1578,9 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     const bool fin = primary && ph == 2;
     const uint32_t sb = copy0_bcast<kE>((uint32_t)st | ((uint32_t)fin << 31));
     const int stc = (int)(sb & 0x7FFFFFFFu);
-    if ((sb >> 31) && (stc & 1) == 0)
+    if ((sb >> 31) && (stc % kCopies) == 0)
       u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + stc + 1 + half);
-    const uint32_t u_next = __shfl(u_drawn, el + kE * (stc & 1));
+    const uint32_t u_next = kCopies == 1 ? u_drawn : (uint32_t)__shfl((int)u_drawn, el + kE * (stc % kCopies));
     // 4. finalize every env whose hand is known (rollout_kernel's finalize)
     if (fin) {
       masks_of(t, s.B, s.hand, m);

@@ -34,6 +34,17 @@ VARIANTS = {
     "apool": ["-DBB_ASYNC_POOL=1"],
     "apool0": ["-DBB_ASYNC_POOL=0"],
     "alate": ["-DBB_ASYNC_LATEPOLL=1"],
+    "ae64": ["-DBB_ASYNC_ENVS=64"],
+    "ae32": ["-DBB_ASYNC_ENVS=32"],
+    "ae64sw2": ["-DBB_ASYNC_SW=2"],
+    "ae64sw3": ["-DBB_ASYNC_SW=3"],
+    "ae64f0": ["-DBB_ASYNC_FAIR=0"],
+    "ae64sp2": ["-DBB_ASYNC_SPRIO=2"],
+    "ae64s1d": ["-DBB_ASYNC_SLOTS64=1"],
+    "ae64s3": ["-DBB_ASYNC_SLOTS64=3"],
+    "ae64sw8": ["-DBB_ASYNC_ENVS=64", "-DBB_ASYNC_SW=8"],
+    "ae64sw6": ["-DBB_ASYNC_ENVS=64", "-DBB_ASYNC_SW=6"],
+    "ae64s1": ["-DBB_ASYNC_ENVS=64", "-DBB_ASYNC_SLOTS64=1"],
     "alatediag": ["-DBB_ASYNC_LATEPOLL=1", "-DBB_ASYNC_DIAG=1"],
     "apsw8": ["-DBB_ASYNC_SW=8"],
     "apsw2": ["-DBB_ASYNC_SW=2"],
