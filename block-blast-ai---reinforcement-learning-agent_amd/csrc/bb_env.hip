@@ -1261,7 +1261,9 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
                          // 0: search wave s serves env waves 2s, 2s+1 (9.60e9 vs 9.89e9 pooled)
 #endif
 #ifndef BB_ASYNC_FAIR
-#define BB_ASYNC_FAIR 1  // env waves: the one behind its SIMD partner takes s_setprio 1 (0: no priority)
+// env waves: the one behind its SIMD partner takes s_setprio 1 (0: no priority).  With 64-env waves each SIMD
+// holds one env wave, so there is no partner: off (1.093e10 vs 1.076e10 with the LDS counters kept)
+#define BB_ASYNC_FAIR (BB_ASYNC_ENVS == 32)
 #endif
 #ifndef BB_ASYNC_SLOTS
 #define BB_ASYNC_SLOTS 1  // in-lane quick-test slots per copy (copy c tests slots c * n .. c * n + n - 1)

@@ -24,7 +24,8 @@ from runtime.device_env import DeviceEnvBatch  # noqa: E402
 def main():
     n = int(os.environ.get("N", "65536"))
     T = int(os.environ.get("T", "128"))
-    ew, sw = int(os.environ.get("EW", "8")), int(os.environ.get("SW", "4"))
+    epw = int(os.environ.get("E", "64"))  # envs per env wave (BB_ASYNC_ENVS)
+    ew, sw = int(os.environ.get("EW", str(256 // epw))), int(os.environ.get("SW", "4"))
     dev = torch.device("cuda", 0)
     env = DeviceEnvBatch(n, seeds=[42 + i for i in range(n)], device=dev)
     env.reset()
@@ -36,8 +37,9 @@ def main():
     term = torch.zeros((T, n), dtype=torch.uint8, device=dev)
     buf = np.zeros((n, 4), dtype=np.uint64)
     out = []
-    nwe = (n + 31) // 32
-    nws = (n + 32 * ew - 1) // (32 * ew) * sw
+    nwe = (n + epw - 1) // epw
+    soff = (n + 31) // 32  # the kernel writes the search waves' counters from here
+    nws = (n + epw * ew - 1) // (epw * ew) * sw
     for call in range(4):
         env.rollout(T, act[0], rew, term, next_action=act[1], policy_step0=call * T)
         act.reverse()
@@ -45,7 +47,7 @@ def main():
         env.lib.bb_debug_counters(env.handle, buf.ctypes.data_as(C.c_void_p))
         flat = buf.reshape(-1)
         we = flat[: 4 * nwe].reshape(-1, 4).astype(np.float64)
-        ws = flat[4 * nwe: 4 * (nwe + nws)].reshape(-1, 4).astype(np.float64)
+        ws = flat[4 * soff: 4 * (soff + nws)].reshape(-1, 4).astype(np.float64)
         out.append({
             "call": call, "T": T,
             "env_iters_per_step": round(we[:, 0].mean() / T, 4),
@@ -53,7 +55,7 @@ def main():
             "env_cyc_per_iter": round(we[:, 1].sum() / we[:, 0].sum(), 1),
             "env_wave_cyc_mean": round(we[:, 1].mean(), 0),
             "env_wave_cyc_max": int(we[:, 1].max()),
-            "blocked_envs_per_iter": round(we[:, 2].sum() / we[:, 0].sum(), 3),
+            "blocked_envs_per_iter_per_wave": round(we[:, 2].sum() / we[:, 0].sum(), 3),
             "idle_iters_per_wave": round(we[:, 3].mean(), 2),
             "search_calls_per_wave": round(ws[:, 0].mean(), 1),
             "envs_per_call": round(ws[:, 1].sum() / max(ws[:, 0].sum(), 1), 2),
