@@ -157,6 +157,9 @@ def main() -> None:
                     torch.zeros((T, ns, 3), dtype=torch.int64, device=dev))
         shards.append((e, torch.cuda.Stream(dev) if S > 1 else torch.cuda.current_stream(dev), a, outs))
     step_idx = [0]
+    # diagnostics only, never the bench line's contract: the launch without the lines / action / mask outputs,
+    # to price the scattered [step][env] stores of the async rollout
+    diag_min_out = os.environ.get("BB_BENCH_MIN_OUTPUTS") == "1"
 
     def one_step(k=1):
         """k bench steps: k bb_step launches (step mode) or k bb_rollout launches of T env-steps each."""
@@ -172,6 +175,8 @@ def main() -> None:
                         e.step(a[0], next_action=a[1], policy_seed=POLICY_SEED, policy_step=t + j + 1)
                     else:
                         o_rew, o_term, o_lines, o_act, o_mask = outs
+                        if diag_min_out:  # diagnostics only (BB_BENCH_MIN_OUTPUTS=1): reward + terminated
+                            o_lines = o_act = o_mask = None
                         e.rollout(T, a[0], o_rew, o_term, lines=o_lines, actions_out=o_act, mask_out=o_mask,
                                   next_action=a[1], policy_seed=POLICY_SEED, policy_step0=t + j * T)
                 a.reverse()
