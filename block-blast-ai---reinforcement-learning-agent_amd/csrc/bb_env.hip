@@ -1271,6 +1271,18 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 #ifndef BB_ASYNC_SLOTS64
 #define BB_ASYNC_SLOTS64 2  // 64-env waves: in-lane quick-test slots per env (0, 1: the two copies' slots)
 #endif
+#ifndef BB_ASYNC_PTOP
+#define BB_ASYNC_PTOP 0  // 64-env waves: the policy uniform drawn at the top of every iteration
+#endif
+#ifndef BB_ASYNC_DEARLY
+#define BB_ASYNC_DEARLY 0  // attempt 1's three draws made for every lane before the move
+#endif
+#ifndef BB_ASYNC_LINEONLY
+#define BB_ASYNC_LINEONLY 0  // search waves: slow_phase_wave's line-only second order (bb_step's kLineOnly)
+#endif
+#ifndef BB_ASYNC_STEP
+#define BB_ASYNC_STEP 0  // bb_step (T = 1, no info / fp64 reward) through rollout_async_kernel
+#endif
 #ifndef BB_ASYNC_LATEPOLL
 #define BB_ASYNC_LATEPOLL 1  // env waves poll their posted envs after the moves (0: before them; 1.017e10 vs 9.89e9)
 #endif
@@ -1281,8 +1293,7 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 #define BB_ASYNC_SLEEP 1  // s_sleep of an idle search wave between polls
 #endif
 constexpr int kAEW = BB_ASYNC_EW, kASW = BB_ASYNC_SW;
-constexpr int kAServe = kAEW / kASW;  // env waves per search wave
-static_assert(BB_ASYNC_POOL || (kAEW % kASW == 0 && (kAServe == 1 || kAServe == 2)), "a search wave serves <= 64 envs");
+static_assert(kAEW % kASW == 0 || kASW % kAEW == 0 || BB_ASYNC_POOL, "search waves split the env waves");
 constexpr int kABlock = 64 * (kAEW + kASW);
 constexpr int kAE = BB_ASYNC_ENVS;
 static_assert(kAE == 32 || kAE == 64, "async env waves: 32 or 64 envs");
@@ -1319,50 +1330,46 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
   stage_tables<true>(t, g_rows, g_d, jt, a.jump);  // ends with __syncthreads (also orders the inits above)
 
   if (wv >= kAEW) {
-    // ---------------- search wave: serves env waves sw * kAServe .. + kAServe - 1 ----------------
+    // ---------------- search wave ----------------
     const int sw = wv - kAEW;
     Pcg rng;
     rng.hi = rng.lo = 0ull;
     rng.buf = 0u;
     rng.has = 0u;
     rng.inc_hi = rng.inc_lo = 0ull;
-#if BB_ASYNC_POOL
-    constexpr int kPer = kAEnvs / 64;  // records watched per lane: k * 64 + lane
+    // pooled claims for rollouts; a single step (bb_step) keeps each search wave on its own env waves'
+    // records, so that the step's parked envs are spread over the search waves instead of one taking all
+    const bool pool = BB_ASYNC_POOL && r.steps > 1;
+    constexpr int kPer = kAEnvs / 64;  // pool: records watched per lane, k * 64 + lane
     static_assert(kAEnvs % 64 == 0, "pool: whole records per lane");
-    int rid = lane;
-#else
-    const int rid = sw * kAServe * 32 + lane;  // the record this lane watches
-    const bool mine = lane < 32 * kAServe;
-    const int gi = blockIdx.x * kAEnvs + rid;
-    if (mine && gi < e.n) {
-      rng.inc_hi = e.inc_hi[gi];
-      rng.inc_lo = e.inc_lo[gi];
-    }
-#endif
+    constexpr int kOwn = kAEnvs / kASW;  // own records per search wave (no pool)
+    static_assert(kOwn <= 64, "a search wave serves <= 64 envs");
+    int rid = pool ? lane : sw * kOwn + lane;
+    const bool mine = lane < kOwn;
     uint64_t B = 0ull;
 #if BB_ASYNC_DIAG  // diagnostics (BB_DEBUG_MODE=16): calls, envs served, search cycles, polls
     uint64_t dcalls = 0, denvs = 0, dcyc = 0, dpolls = 0;
 #endif
 #pragma unroll 1
     for (;;) {
-#if BB_ASYNC_POOL
-      // claim the first posted record among this lane's (posted -> 3 by compare-and-swap)
       uint32_t sv = 0u;
+      if (pool) {
+        // claim the first posted record among this lane's (posted -> 3 by compare-and-swap)
 #pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        if (sv != 1u &&
-            __hip_atomic_load(&astat[k * 64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u) {
-          uint32_t expect = 1u;
-          if (__hip_atomic_compare_exchange_strong(&astat[k * 64 + lane], &expect, 3u, __ATOMIC_RELAXED,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            sv = 1u;
-            rid = k * 64 + lane;
+        for (int k = 0; k < kPer; ++k) {
+          if (sv != 1u &&
+              __hip_atomic_load(&astat[k * 64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u) {
+            uint32_t expect = 1u;
+            if (__hip_atomic_compare_exchange_strong(&astat[k * 64 + lane], &expect, 3u, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              sv = 1u;
+              rid = k * 64 + lane;
+            }
           }
         }
+      } else if (mine) {
+        sv = __hip_atomic_load(&astat[rid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-#else
-      const uint32_t sv = mine ? __hip_atomic_load(&astat[rid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
-#endif
       const uint64_t req = __ballot(sv == 1u);
       if (req) {
         wave_lds_fence();
@@ -1373,17 +1380,16 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
           rng.lo = R.lo;
           rng.buf = R.buf;
           rng.has = R.has_ids & 1u;
-#if BB_ASYNC_POOL
           rng.inc_hi = R.inc_hi;
           rng.inc_lo = R.inc_lo;
-#endif
         }
         __builtin_amdgcn_s_setprio(BB_ASYNC_SPRIO);
         uint32_t ids = 0;
 #if BB_ASYNC_DIAG
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
-        gen_hands_multi<64, false>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+        gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
+                                                     a.pack_next, lds);
 #if BB_ASYNC_DIAG
         dcyc += __builtin_amdgcn_s_memtime() - c0;
         dcalls += 1;
@@ -1401,11 +1407,9 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         if (sv == 1u) __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
         uint32_t fin = 1u;
-        constexpr int kWatch = BB_ASYNC_POOL ? kAEW : kAServe;  // env waves whose end this wave waits for
 #pragma unroll
-        for (int q = 0; q < kWatch; ++q)
-          fin &= __hip_atomic_load(&afin[BB_ASYNC_POOL ? q : sw * kAServe + q], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int q = 0; q < kAEW; ++q)  // every env wave (a cheap superset of the ones this wave serves)
+          fin &= __hip_atomic_load(&afin[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (fin) break;  // wave-uniform (LDS word read by every lane)
 #if BB_ASYNC_DIAG
         dpolls += 1;
@@ -1519,9 +1523,26 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     // 2. the move of every ready env; a drawn hand is quick-tested by both copies (copy 1 takes the
     //    post-move board and the drawn pieces from copy 0, as in rollout_kernel)
     const bool mv = primary && ph == 0 && st < T;
+    // one lane per env: this step's policy uniform depends only on the step counter, so it is drawn
+    // here, without a branch, and its Philox rounds overlap the move's table reads
+    const uint32_t u_top = (kCopies == 1 && BB_ASYNC_PTOP)
+                               ? policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + st + 1)
+                               : 0u;
     Pcg after = s.rng;
     uint32_t ids0 = 0;
     bool drew0 = false;
+#if BB_ASYNC_DEARLY
+    // attempt 1's draws do not depend on the move: drawn for every lane before it (used where it drew)
+    uint32_t ex0 = 0, ex1 = 0, ex2 = 0;
+    draw3(after, ex0, ex1, ex2);
+    if (mv) {
+      drew0 = apply_move_bf(t, s, act);
+      if (drew0) {
+        ids0 = ex0 | (ex1 << 6) | (ex2 << 12);
+        s.hand = ids0;
+      }
+    }
+#else
     if (mv) {
       drew0 = apply_move_bf(t, s, act);
       if (drew0) {
@@ -1534,6 +1555,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         s.hand = ids0;
       }
     }
+#endif
     const uint32_t idq = copy0_bcast<kE>((uint32_t)ids0 | ((uint32_t)drew0 << 31));
     const uint64_t Bq = ((uint64_t)copy0_bcast<kE>((uint32_t)(s.B >> 32)) << 32) | copy0_bcast<kE>((uint32_t)s.B);
     bool park = false;
@@ -1563,10 +1585,8 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
           R.lo = s.rng.lo;
           R.buf = s.rng.buf;
           R.has_ids = s.rng.has ? 1u : 0u;
-          if (BB_ASYNC_POOL) {
-            R.inc_hi = s.rng.inc_hi;
-            R.inc_lo = s.rng.inc_lo;
-          }
+          R.inc_hi = s.rng.inc_hi;
+          R.inc_lo = s.rng.inc_lo;
           wave_lds_fence();
           __hip_atomic_store(&astat[rid], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           ph = 1;
@@ -1580,9 +1600,10 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     const bool fin = primary && ph == 2;
     const uint32_t sb = copy0_bcast<kE>((uint32_t)st | ((uint32_t)fin << 31));
     const int stc = (int)(sb & 0x7FFFFFFFu);
-    if ((sb >> 31) && (stc % kCopies) == 0)
+    if (!(kCopies == 1 && BB_ASYNC_PTOP) && (sb >> 31) && (stc % kCopies) == 0)
       u_drawn = policy_uniform(a.policy_seed, a.env_offset + (uint64_t)i, r.policy_step0 + stc + 1 + half);
-    const uint32_t u_next = kCopies == 1 ? u_drawn : (uint32_t)__shfl((int)u_drawn, el + kE * (stc % kCopies));
+    const uint32_t u_next = (kCopies == 1 && BB_ASYNC_PTOP) ? u_top
+                          : kCopies == 1 ? u_drawn : (uint32_t)__shfl((int)u_drawn, el + kE * (stc % kCopies));
     // 4. finalize every env whose hand is known (rollout_kernel's finalize)
     if (fin) {
       masks_of(t, s.B, s.hand, m);
@@ -1637,6 +1658,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
       st += 1;
       ph = 0;
     }
+    if (!__ballot(mv || fin)) __builtin_amdgcn_s_sleep(1);  // every env blocked: leave the SIMD to the searches
   }
   __builtin_amdgcn_s_setprio(0);
 #if BB_ASYNC_DIAG
@@ -1791,7 +1813,10 @@ hipError_t launch_step(const EnvDev& e, const PieceRow* rows, const uint8_t* d, 
 hipError_t launch_rollout(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const StepArgs& a,
                           const RollArgs& r, hipStream_t s) {
   auto grid = [&](int epw, int blk) { return dim3((unsigned)((((int64_t)e.n + epw - 1) / epw * 64 + blk - 1) / blk)); };
-  if (r.steps == 1) {  // bb_step
+  if (r.steps == 1 && BB_ASYNC_STEP && !r.info && !r.reward_f64) {  // bb_step through the async kernel
+    const dim3 g((unsigned)(((int64_t)e.n + kAEnvs - 1) / kAEnvs)), b(kABlock);
+    hipLaunchKernelGGL(rollout_async_kernel, g, b, 0, s, e, rows, d, a, r);
+  } else if (r.steps == 1) {  // bb_step
     const dim3 g = grid(kStepEnvs, kStepRollBlock), b(kStepRollBlock);
     if (r.info || r.reward_f64)
       hipLaunchKernelGGL((rollout_kernel<true, true, kStepEnvs, kStepRollBlock>), g, b, 0, s, e, rows, d, a, r);

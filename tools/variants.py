@@ -35,6 +35,15 @@ VARIANTS = {
     "apool0": ["-DBB_ASYNC_POOL=0"],
     "alate": ["-DBB_ASYNC_LATEPOLL=1"],
     "ae64": ["-DBB_ASYNC_ENVS=64"],
+    "aptop": ["-DBB_ASYNC_PTOP=1"],
+    "astep": ["-DBB_ASYNC_STEP=1"],
+    "astep32": ["-DBB_ASYNC_STEP=1", "-DBB_ASYNC_ENVS=32"],
+    "alo": ["-DBB_ASYNC_LINEONLY=1"],
+    "alo256": ["-DBB_ASYNC_LINEONLY=1", "-DBB_SLOW_LINE_MIN=256"],
+    "alo128": ["-DBB_ASYNC_LINEONLY=1", "-DBB_SLOW_LINE_MIN=128"],
+    "asexit0": ["-DBB_SLOW_EXIT=0"],
+    "adearly": ["-DBB_ASYNC_DEARLY=1"],
+    "aptde": ["-DBB_ASYNC_PTOP=1", "-DBB_ASYNC_DEARLY=1"],
     "ae32": ["-DBB_ASYNC_ENVS=32"],
     "ae64sw2": ["-DBB_ASYNC_SW=2"],
     "ae64sw3": ["-DBB_ASYNC_SW=3"],
