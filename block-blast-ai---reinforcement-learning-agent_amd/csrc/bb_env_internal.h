@@ -114,7 +114,12 @@ int64_t conv_in_wgrad_workspace_bytes(int nb);
 hipError_t launch_conv_in_forward(const float* x, const float* w, int wl, int nb, void* y, hipStream_t s);
 hipError_t launch_conv_in_wgrad(const float* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s);
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
-                                  const void* radd = nullptr);
+                                  const void* radd = nullptr, const float* pb = nullptr, double* part = nullptr);
+int conv3x3_stats_parts(int nb, int cout);
+hipError_t launch_bn_forward_parts(const void* x, const void* res, int dtype, int nhwc, int N, int C, int HW,
+                                   const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
+                                   const double* part, int nparts, float* save_mean, float* save_invstd,
+                                   float* rmean, float* rvar, float momentum, int64_t* nbt, void* y, hipStream_t s);
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);
 

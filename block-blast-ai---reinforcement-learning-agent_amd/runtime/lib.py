@@ -144,6 +144,8 @@ SIGNATURES = {
                                 _P]),
     "bb_bn_forward_res": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P,
                                     _F, _P, _P, _P]),
+    "bb_bn_forward_parts": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _I32, _P,
+                                      _P, _P, _P, _F, _P, _P, _P]),
     "bb_bn_backward": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                  _P]),
     "bb_conv3x3_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
@@ -151,6 +153,8 @@ SIGNATURES = {
     "bb_conv3x3_prep_multi": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P]),
     "bb_conv3x3_forward": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_conv3x3_forward_add": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
+    "bb_conv3x3_stats_parts": (C.c_int64, [_I32, _I32]),
+    "bb_conv3x3_forward_stats": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     "bb_conv3x3_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _P, _P]),
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),
     "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),

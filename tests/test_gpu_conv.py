@@ -265,3 +265,117 @@ def test_network_bf16_step_deterministic(cuda, lib, monkeypatch):
         outs.append([lo.detach(), va.detach()] + [p.grad.clone() for p in net.parameters()])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("cin,cout", SHAPES)
+@pytest.mark.parametrize("n", [1, 3, 257, 2048])
+def test_conv3x3_forward_stats(cuda, lib, cin, cout, n):
+    """bb_conv3x3_forward_stats: the same y as bb_conv3x3_forward, and per channel the fp64 sums of
+    u = y + pre_bias and u^2 over every pixel (BatchNorm's forward statistics) equal to a float64
+    reduction of the stored values; bit-identical on a second call."""
+    from runtime.kernels import _p, _s
+
+    x, w, _ = _inputs(cuda, n, cin, cout, 300 + n + cin + cout, layout=0)
+    wf = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=cuda)
+    wd = torch.empty_like(wf)
+    assert lib.bb_conv3x3_prep(_p(w), cin, cout, 0, _p(wf), _p(wd), _s(cuda)) == 0
+    pb = torch.randn(cout, device=cuda)
+    y0 = torch.empty((n, cout, 8, 8), dtype=torch.bfloat16, device=cuda, memory_format=torch.channels_last)
+    assert lib.bb_conv3x3_forward(_p(x), _p(wf), n, cin, cout, _p(y0), _s(cuda)) == 0
+    nparts = lib.bb_conv3x3_stats_parts(n, cout)
+    assert nparts >= 1
+    outs = []
+    for _ in range(2):
+        y = torch.empty_like(y0)
+        part = torch.full((nparts, cout, 3), float("nan"), dtype=torch.float64, device=cuda)
+        assert lib.bb_conv3x3_forward_stats(_p(x), _p(wf), n, cin, cout, _p(y), _p(pb), _p(part), _s(cuda)) == 0
+        outs.append((y, part))
+    torch.cuda.synchronize()
+    (y, part), (y2, part2) = outs
+    assert torch.equal(y, y0) and torch.equal(y2, y0)
+    assert torch.equal(part, part2)
+    u = (y.float() + pb.view(1, -1, 1, 1)).double()
+    s_ref = u.sum(dim=(0, 2, 3))
+    q_ref = (u * u).sum(dim=(0, 2, 3))
+    s = part[:, :, 0].sum(0)
+    q = part[:, :, 1].sum(0)
+    assert torch.allclose(s, s_ref, rtol=1e-12, atol=1e-9 * float(s_ref.abs().max()))
+    assert torch.allclose(q, q_ref, rtol=1e-12, atol=0)
+    assert bool((part[:, :, 2] == 0).all())
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (False, True)])
+def test_bn_forward_from_conv_stats(cuda, lib, relu, res):
+    """bb_bn_forward_parts (statistics from the convolution's epilogue) against bb_bn_forward[_res]
+    (its own reduction pass) on the same convolution output: mean / inverse std / running statistics
+    within f32 rounding, the output within one bf16 step, num_batches_tracked incremented."""
+    from runtime.kernels import BatchNormAddReLUFunction, BatchNormReLUFunction, Conv3x3Function
+
+    n, c = 2048, 128
+    x, w, _ = _inputs(cuda, n, 64, c, 7, layout=0)
+    pb = torch.randn(c, device=cuda) * 0.1
+    parts = torch.empty((lib.bb_conv3x3_stats_parts(n, c), c, 3), dtype=torch.float64, device=cuda)
+    z = Conv3x3Function.apply(x, w, None, None, (pb, parts))
+    r = torch.randn_like(z) if res else None
+    outs = []
+    for use in (None, parts):
+        bn = torch.nn.BatchNorm2d(c).to(cuda)
+        with torch.no_grad():  # the same affine parameters for both
+            bn.weight.copy_(torch.linspace(0.5, 1.5, c, device=cuda))
+            bn.bias.copy_(torch.linspace(-0.2, 0.2, c, device=cuda))
+        if res:
+            y = BatchNormAddReLUFunction.apply(z, pb, r, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                               0.1, 1e-5, bn.num_batches_tracked, None, use)
+        else:
+            y = BatchNormReLUFunction.apply(z, pb, bn.weight, bn.bias, bn.running_mean, bn.running_var, 0.1, 1e-5,
+                                            relu, bn.num_batches_tracked, use)
+        outs.append((y, bn))
+    (y0, bn0), (y1, bn1) = outs
+    assert int(bn1.num_batches_tracked) == 1
+    assert torch.allclose(bn1.running_mean, bn0.running_mean, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(bn1.running_var, bn0.running_var, rtol=1e-5, atol=1e-7)
+    _bf16_close(y1.detach(), y0.detach().float(), "BatchNorm output from the conv statistics")
+
+
+def test_network_bf16_conv_stats_matches_reduction(cuda, lib, monkeypatch):
+    """The whole CNN's bf16 training forward + backward with the BatchNorm statistics from the
+    convolution epilogues (BB_CONV_BN_STATS, shipped) against the BatchNorm's own reduction passes:
+    logits, values and every parameter gradient within a relative L2 of 2e-2 (bf16 activations: a
+    statistic that differs in its last f32 bit can move an element by one bf16 step), running
+    statistics within 1e-5."""
+    import models.network as NW
+    from models.network import BlockBlastNetwork
+
+    torch.manual_seed(6)
+    nets = [BlockBlastNetwork().to(cuda).train().to(memory_format=torch.channels_last) for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    for net in nets:
+        for m in net.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+    x = (torch.rand((1024, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for net, on in zip(nets, (True, False)):
+        monkeypatch.setattr(NW, "CONV_BN_STATS", on)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            lo, va = net.raw(x)
+        (lo.float().square().mean() + va.float().sum()).backward()
+        outs.append((lo.detach().float(), va.detach().float(), {k: p.grad for k, p in net.named_parameters()},
+                     {k: b for k, b in net.named_buffers()}))
+
+    def rel(a, b):
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+    (l1, v1, g1, b1), (l0, v0, g0, b0) = outs
+    assert rel(l1, l0) < 2e-2 and rel(v1, v0) < 2e-2
+    for k in g0:
+        if g0[k] is None or float(g0[k].norm()) == 0.0:
+            continue
+        if k.endswith(".bias") and dict(nets[0].named_parameters())[k[:-5] + ".weight"].dim() == 4:
+            continue  # conv biases feed a BatchNorm: true gradient 0
+        assert rel(g1[k], g0[k]) < 2e-2, k
+    for k in b0:
+        if b0[k].dtype.is_floating_point:
+            assert torch.allclose(b1[k], b0[k], rtol=1e-5, atol=1e-6), k
+        else:
+            assert torch.equal(b1[k], b0[k]), k
