@@ -1482,13 +1482,18 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
   int ph = 0;   // copy 0: 0 ready to move, 1 posted (blocked), 2 hand known (finalize)
   uint32_t u_drawn = 0;
   uint32_t partner = 0;
-  const int cap = 4 * T + 4096;  // iterations: T plus the blocked ones; far above any real count
+  // Bounds (never reached by a correct run): an iteration that moves or finalizes some env advances one of the
+  // wave's 2 * kE * T phases, so there are at most 2 * kE * T of them; iterations in which every unfinished env
+  // waits on a search last as long as that search (at most 100 attempts), so 2^24 of them (seconds) means a
+  // lost record -- the wave then ends instead of hanging the GPU.
+  const int64_t cap = 2 * (int64_t)kE * T + 4096;
+  int64_t work_it = 0, idle_it = 0;
 #if BB_ASYNC_DIAG  // iterations, cycles, blocked env-iterations, iterations that moved no env
   uint64_t dit = 0, dblk = 0, didle = 0;
   const uint64_t dt0 = __builtin_amdgcn_s_memtime();
 #endif
 #pragma unroll 1
-  for (int it = 0; it < cap; ++it) {
+  for (int it = 0; work_it < cap && idle_it < (1 << 24); ++it) {
     if (!__ballot(primary && st < T)) break;
 #if BB_ASYNC_DIAG
     dit += 1;
@@ -1658,7 +1663,12 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
       st += 1;
       ph = 0;
     }
-    if (!__ballot(mv || fin)) __builtin_amdgcn_s_sleep(1);  // every env blocked: leave the SIMD to the searches
+    if (!__ballot(mv || fin)) {  // every env blocked: leave the SIMD to the searches
+      ++idle_it;
+      __builtin_amdgcn_s_sleep(1);
+    } else {
+      ++work_it;
+    }
   }
   __builtin_amdgcn_s_setprio(0);
 #if BB_ASYNC_DIAG
