@@ -69,8 +69,9 @@ PREP_MULTI = os.environ.get("BB_PREP_MULTI", "1") != "0"  # the HIP convs' weigh
 RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass
 # ... and the identity path's input gradient added in conv1's data-gradient store pass (no add kernel)
 RES_GRAD_FUSED = os.environ.get("BB_RES_GRAD_FUSED", "1") != "0"
-# the BatchNorm forward statistics of a HIP convolution's output summed in its epilogue (no reduction pass)
-CONV_BN_STATS = os.environ.get("BB_CONV_BN_STATS", "1") != "0"
+# the BatchNorm forward statistics of a HIP convolution's output summed in its epilogue (no reduction pass):
+# parity-tested, measured slower and opt-in (bf16 update step 1.851 vs 1.840 ms, profiles/r03/bns/)
+CONV_BN_STATS = os.environ.get("BB_CONV_BN_STATS", "0") == "1"
 
 
 def _hip_conv_on(x: torch.Tensor) -> bool:

@@ -334,46 +334,61 @@ def test_bn_forward_from_conv_stats(cuda, lib, relu, res):
     assert int(bn1.num_batches_tracked) == 1
     assert torch.allclose(bn1.running_mean, bn0.running_mean, rtol=1e-5, atol=1e-7)
     assert torch.allclose(bn1.running_var, bn0.running_var, rtol=1e-5, atol=1e-7)
-    _bf16_close(y1.detach(), y0.detach().float(), "BatchNorm output from the conv statistics")
+    if not res:
+        _bf16_close(y1.detach(), y0.detach().float(), "BatchNorm output from the conv statistics")
+    else:  # relu(round(bn) + res), rounded again: one bf16 step of the BatchNorm value before the add and one
+        # of the sum after it
+        a, b = y1.detach().float(), y0.detach().float()
+        bad = (a - b).abs() > 2.0 ** -7 * (2 * b.abs() + r.float().abs()) + 1e-6
+        assert int(bad.sum()) == 0, f"{int(bad.sum())} residual-path elements off by more than one bf16 step"
+        assert float((a == b).float().mean()) > 0.97
 
 
 def test_network_bf16_conv_stats_matches_reduction(cuda, lib, monkeypatch):
     """The whole CNN's bf16 training forward + backward with the BatchNorm statistics from the
-    convolution epilogues (BB_CONV_BN_STATS, shipped) against the BatchNorm's own reduction passes:
-    logits, values and every parameter gradient within a relative L2 of 2e-2 (bf16 activations: a
-    statistic that differs in its last f32 bit can move an element by one bf16 step), running
-    statistics within 1e-5."""
+    convolution epilogues (BB_CONV_BN_STATS=1) and with the BatchNorm's own reduction passes,
+    both against the f32 network: the fused path is as close to f32 as the unfused one (logits, values,
+    every parameter gradient, relative L2 <= 1.5x + 2e-3 -- the first convolution's gradient is a
+    difference of near-equal terms behind a BatchNorm and MIOpen's weight gradient is not deterministic,
+    so a direct comparison of the two bf16 runs is not meaningful there), running statistics within 1e-5."""
     import models.network as NW
     from models.network import BlockBlastNetwork
 
     torch.manual_seed(6)
-    nets = [BlockBlastNetwork().to(cuda).train().to(memory_format=torch.channels_last) for _ in range(2)]
-    nets[1].load_state_dict(nets[0].state_dict())
+    nets = [BlockBlastNetwork().to(cuda).train().to(memory_format=torch.channels_last) for _ in range(3)]
+    for m in nets[1:]:
+        m.load_state_dict(nets[0].state_dict())
     for net in nets:
         for m in net.modules():
             if isinstance(m, torch.nn.Dropout):
                 m.p = 0.0
     x = (torch.rand((1024, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    wgt = None
     outs = []
-    for net, on in zip(nets, (True, False)):
-        monkeypatch.setattr(NW, "CONV_BN_STATS", on)
-        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+    for net, mode in zip(nets, ("stats", "reduce", "f32")):
+        monkeypatch.setattr(NW, "CONV_BN_STATS", mode == "stats")
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False, enabled=mode != "f32"):
             lo, va = net.raw(x)
-        (lo.float().square().mean() + va.float().sum()).backward()
-        outs.append((lo.detach().float(), va.detach().float(), {k: p.grad for k, p in net.named_parameters()},
+        lo, va = lo.float(), va.float()
+        if wgt is None:
+            wgt = torch.randn_like(lo)
+        ((lo * wgt).sum() + va.sum()).backward()
+        outs.append((lo.detach(), va.detach(), {k: p.grad for k, p in net.named_parameters()},
                      {k: b for k, b in net.named_buffers()}))
 
     def rel(a, b):
         return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
-    (l1, v1, g1, b1), (l0, v0, g0, b0) = outs
-    assert rel(l1, l0) < 2e-2 and rel(v1, v0) < 2e-2
-    for k in g0:
-        if g0[k] is None or float(g0[k].norm()) == 0.0:
-            continue
-        if k.endswith(".bias") and dict(nets[0].named_parameters())[k[:-5] + ".weight"].dim() == 4:
+    (l1, v1, g1, b1), (l0, v0, g0, b0), (l32, v32, g32, _) = outs
+    rows = [("logits", rel(l1, l32), rel(l0, l32)), ("values", rel(v1, v32), rel(v0, v32))]
+    params = dict(nets[2].named_parameters())
+    for k in g32:
+        if k.endswith(".bias") and params[k].dim() == 1 and params[k[:-5] + ".weight"].dim() == 4:
             continue  # conv biases feed a BatchNorm: true gradient 0
-        assert rel(g1[k], g0[k]) < 2e-2, k
+        rows.append((k, rel(g1[k], g32[k]), rel(g0[k], g32[k])))
+    table = "\n".join(f"{n:40s} stats {a:.4f} reduce {b:.4f}" for n, a, b in rows)
+    for name, a, b in rows:
+        assert a <= 1.5 * b + 2e-3, f"{name}: conv-statistics error {a:.4f} vs reduction {b:.4f}\n{table}"
     for k in b0:
         if b0[k].dtype.is_floating_point:
             assert torch.allclose(b1[k], b0[k], rtol=1e-5, atol=1e-6), k
