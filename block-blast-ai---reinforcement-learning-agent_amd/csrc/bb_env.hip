@@ -1283,6 +1283,9 @@ __global__ void __launch_bounds__(kBlock, BB_ROLL_MINW) rollout_kernel(EnvDev e,
 #ifndef BB_ASYNC_STEP
 #define BB_ASYNC_STEP 0  // bb_step (T = 1, no info / fp64 reward) through rollout_async_kernel
 #endif
+#ifndef BB_ASYNC_EARLY
+#define BB_ASYNC_EARLY 1  // search waves hand back each env when its round decides it, not at the call's end (1.105e10 vs 1.076e10)
+#endif
 #ifndef BB_ASYNC_LATEPOLL
 #define BB_ASYNC_LATEPOLL 1  // env waves poll their posted envs after the moves (0: before them; 1.017e10 vs 9.89e9)
 #endif
@@ -1388,15 +1391,34 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
 #if BB_ASYNC_DIAG
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
+        bool released = false;
+#if BB_ASYNC_EARLY
+        // envs decided in an earlier round of the call go back to their env waves at once
+        auto release = [&](bool d) {
+          if (d && sv == 1u) {
+            ARec& R = arec[rid];
+            R.hi = rng.hi;
+            R.lo = rng.lo;
+            R.buf = rng.buf;
+            R.has_ids = (rng.has ? 1u : 0u) | (ids << 1);
+            wave_lds_fence();
+            __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            released = true;
+          }
+        };
+        gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
+                                                     a.pack_next, lds, nullptr, 0, release);
+#else
         gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
                                                      a.pack_next, lds);
+#endif
 #if BB_ASYNC_DIAG
         dcyc += __builtin_amdgcn_s_memtime() - c0;
         dcalls += 1;
         denvs += (uint64_t)__popcll(req);
 #endif
         __builtin_amdgcn_s_setprio(0);
-        if (sv == 1u) {
+        if (sv == 1u && !released) {
           ARec& R = arec[rid];
           R.hi = rng.hi;
           R.lo = rng.lo;
@@ -1404,7 +1426,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
           R.has_ids = (rng.has ? 1u : 0u) | (ids << 1);
         }
         wave_lds_fence();
-        if (sv == 1u) __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (sv == 1u && !released) __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
         uint32_t fin = 1u;
 #pragma unroll

@@ -867,12 +867,19 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
 // packed (all failed) attempts.  The first attempt lane is always packed, so
 // every round makes progress.
 // ---------------------------------------------------------------------------
-template <int kEnvs, bool kLineOnly = false>
+struct NoRelease {
+  __device__ void operator()(bool) const {}
+};
+
+// release(done): called after every round with done set in the lanes of the envs that round decided (their
+// rng / ids are final), so a caller can hand them on before the other envs' later rounds
+template <int kEnvs, bool kLineOnly = false, typename Release = NoRelease>
 __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pcg& rng, uint32_t& ids,
                                                 const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
                                                 int lane, int pack_first, int pack_next, uint32_t* lds,
                                                 uint64_t* prof = nullptr,  // diagnostics: [6] cycle sums
-                                                int att0 = 0) {  // attempts an earlier pass consumed (env lanes)
+                                                int att0 = 0,  // attempts an earlier pass consumed (env lanes)
+                                                const Release& release = Release()) {
 #define BB_MT(x) const uint64_t x = prof ? __builtin_amdgcn_s_memtime() : 0
   const int me = lane % kEnvs;  // env index held by this lane
   int att = att0;             // attempts consumed so far (env lanes)
@@ -925,6 +932,7 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
         rng = w;
         ids = wids;
       }
+      release(me == e0);
       todo &= todo - 1;
       continue;
     }
@@ -1084,6 +1092,7 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       }
     }
     todo &= ~(__ballot(done && lane < kEnvs) & (kEnvs >= 64 ? ~0ull : ((1ull << (kEnvs & 63)) - 1ull)));
+    release(done && lane < kEnvs);
     pk = pack_next > 0 ? pack_next : 2 * pk;
     pk = pk < kPack ? pk : kPack;
     if (prof) {

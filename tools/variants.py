@@ -36,9 +36,9 @@ VARIANTS = {
     "alate": ["-DBB_ASYNC_LATEPOLL=1"],
     "ae64": ["-DBB_ASYNC_ENVS=64"],
     "aptop": ["-DBB_ASYNC_PTOP=1"],
-    # search waves hand back each env when its round decides it (tools/patches/async_early.diff: not GPU-measured
-    # yet; apply the patch to rebuild this)
+    # search waves hand back each env when its round decides it (shipped; "aearly0" is the call-end hand-back)
     "aearly": ["-DBB_ASYNC_EARLY=1"],
+    "aearly0": ["-DBB_ASYNC_EARLY=0"],
     "astep": ["-DBB_ASYNC_STEP=1"],
     "astep32": ["-DBB_ASYNC_STEP=1", "-DBB_ASYNC_ENVS=32"],
     "alo": ["-DBB_ASYNC_LINEONLY=1"],
