@@ -39,6 +39,8 @@ struct bb_env {
   // bb_step through the rollout kernel (T = 1) instead of step + escalate kernels; the latter serves the
   // diagnostic modes (BB_DEBUG_MODE, BB_LANE_BUDGET, BB_LANE_QUICK) and BB_STEP_KERNELS=2
   bool fused_step = true;
+  uint32_t* h_status = nullptr;  // device failure word (pinned, device-mapped): EnvDev::status, see kStatus*
+  int64_t work_cap = 0;          // BB_DEBUG_ASYNC_CAP: rollout_async_kernel's working-iteration cap (tests only)
   std::string err;
 };
 
@@ -61,6 +63,20 @@ int fail(bb_env* e, int code, const std::string& msg) {
 
 int hip_fail(bb_env* e, hipError_t st, const char* what) {
   return fail(e, BB_ERR_HIP, std::string(what) + ": " + hipGetErrorString(st));
+}
+
+// A kernel raised the handle's status word (EnvDev::status): an earlier launch's outputs and the env state are
+// incomplete.  The handle refuses work until a full bb_reset.  Reads the pinned word without synchronising, so
+// it sees the launches that have finished by now (bb_sync waits for them first).
+int status_fail(bb_env* e, const char* what) {
+  const uint32_t st = __atomic_load_n(e->h_status, __ATOMIC_ACQUIRE);
+  if (st == 0u) return BB_OK;
+  e->broken = true;
+  std::string why = st == kStatusAsyncCap
+                        ? "a wave of rollout_async_kernel left through its iteration cap (a lost hand-search record): "
+                          "that bb_rollout's outputs and the env state are incomplete"
+                        : "device status " + std::to_string(st);
+  return fail(e, BB_ERR_DEVICE, std::string(what) + ": " + why + "; call bb_reset on all envs (d_env_mask = NULL)");
 }
 
 struct DeviceGuard {
@@ -214,6 +230,19 @@ int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg, int32_
     delete e;
     return fail(nullptr, BB_ERR_HIP, m);
   }
+  if (const char* s = getenv("BB_DEBUG_ASYNC_CAP")) e->work_cap = atoll(s) > 0 ? atoll(s) : 0;
+  st = hipHostMalloc(reinterpret_cast<void**>(&e->h_status), 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (st == hipSuccess) {
+    *e->h_status = 0u;
+    st = hipHostGetDevicePointer(reinterpret_cast<void**>(&d.status), e->h_status, 0);
+  }
+  if (st != hipSuccess) {
+    std::string m = std::string("bb_create: status word: ") + hipGetErrorString(st);
+    if (e->h_status) (void)hipHostFree(e->h_status);
+    (void)hipFree(e->slab);
+    delete e;
+    return fail(nullptr, BB_ERR_HIP, m);
+  }
   if (e->dbg & 30) {
     if (hipMalloc(&e->dbg_out, n * 32) != hipSuccess) e->dbg &= ~30;
     else (void)hipMemset(e->dbg_out, 0, n * 32);
@@ -230,6 +259,7 @@ void bb_destroy(bb_env* env) {
     (void)hipFree(env->slab);
   }
   if (env->dbg_out) (void)hipFree(env->dbg_out);
+  if (env->h_status) (void)hipHostFree(env->h_status);
   delete env;
 }
 
@@ -275,10 +305,17 @@ int bb_seed(bb_env* env, const uint64_t* h_seeds, const uint8_t* h_has_seed, con
 int bb_reset(bb_env* env, const uint8_t* d_env_mask, void* stream) {
   if (!env) return BB_ERR_ARG;
   if (env->broken && d_env_mask) return broken_fail(env, "bb_reset (masked)");
+  if (d_env_mask && status_fail(env, "bb_reset (masked)") != BB_OK) return BB_ERR_DEVICE;
   DeviceGuard g(env->device);
-  hipError_t st = launch_reset(env->d, env->d_rows, env->d_dtab, d_env_mask, (hipStream_t)stream);
+  hipError_t st = hipSuccess;
+  if (!d_env_mask && (env->broken || __atomic_load_n(env->h_status, __ATOMIC_ACQUIRE))) {
+    // a failed launch may still be running: let it finish before its status word is cleared
+    st = hipStreamSynchronize((hipStream_t)stream);
+    __atomic_store_n(env->h_status, 0u, __ATOMIC_RELEASE);
+  }
+  if (st == hipSuccess) st = launch_reset(env->d, env->d_rows, env->d_dtab, d_env_mask, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(env, st, "bb_reset");
-  env->broken = false;  // every env reset, every pend flag cleared
+  if (!d_env_mask) env->broken = false;  // every env reset, every pend flag cleared
   return BB_OK;
 }
 
@@ -300,6 +337,7 @@ int bb_step(bb_env* env, const int32_t* d_actions, const bb_step_out* out, void*
   a.final_score = out->final_score;
   a.final_moves = out->final_moves;
   DeviceGuard g(env->device);
+  if (status_fail(env, "bb_step") != BB_OK) return BB_ERR_DEVICE;
   if (env->broken) return broken_fail(env, "bb_step");
   hipError_t st;
   if (env->fused_step) {
@@ -335,6 +373,7 @@ int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions, const bb_ro
   if (!d_actions || !out || !out->reward || !out->terminated)
     return fail(env, BB_ERR_ARG, "bb_rollout: actions, reward and terminated are required");
   if (env->dbg & ~16) return fail(env, BB_ERR_STATE, "bb_rollout: only BB_DEBUG_MODE=16 (rollout phase counters)");
+  if (status_fail(env, "bb_rollout") != BB_OK) return BB_ERR_DEVICE;
   if (env->broken) return broken_fail(env, "bb_rollout");
   if (steps == 0) return BB_OK;
   StepArgs a = base_args(env);
@@ -350,10 +389,19 @@ int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions, const bb_ro
   r.mask = out->mask;
   r.next_action = out->next_action;
   r.policy_step0 = out->policy_step0;
+  r.work_cap = env->work_cap;
   DeviceGuard g(env->device);
   hipError_t st = launch_rollout(env->d, env->d_rows, env->d_dtab, a, r, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(env, st, "bb_rollout");
   return BB_OK;
+}
+
+int bb_sync(bb_env* env, void* stream) {
+  if (!env) return BB_ERR_ARG;
+  DeviceGuard g(env->device);
+  const hipError_t st = hipStreamSynchronize((hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(env, st, "bb_sync");
+  return status_fail(env, "bb_sync");
 }
 
 int bb_obs(bb_env* env, float* d_x, int8_t* d_mask_i8, float* d_mask_f32, uint64_t* d_mask_bits, void* stream) {
@@ -398,6 +446,7 @@ int bb_get_state(bb_env* env, const bb_state_view* v) {
   auto cp = [&](void* dst, const void* src, size_t bytes) {
     if (dst && st == hipSuccess) st = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
   };
+  if (st == hipSuccess && status_fail(env, "bb_get_state") != BB_OK) return BB_ERR_DEVICE;
   cp(v->board, env->d.board, n * 8);
   cp(v->hand, env->d.hand, n * 4);
   cp(v->score, env->d.score, n * 8);

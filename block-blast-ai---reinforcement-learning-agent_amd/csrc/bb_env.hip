@@ -1375,7 +1375,8 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
       }
       const uint64_t req = __ballot(sv == 1u);
       if (req) {
-        wave_lds_fence();
+        // acquire: the claimed records' fields were written before their poster's release of status 1
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         if (sv == 1u) {
           const ARec& R = arec[rid];
           B = R.B;
@@ -1401,8 +1402,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
             R.lo = rng.lo;
             R.buf = rng.buf;
             R.has_ids = (rng.has ? 1u : 0u) | (ids << 1);
-            wave_lds_fence();
-            __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            lds_flag_store_release(&astat[rid], 2u);
             released = true;
           }
         };
@@ -1424,9 +1424,8 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
           R.lo = rng.lo;
           R.buf = rng.buf;
           R.has_ids = (rng.has ? 1u : 0u) | (ids << 1);
+          lds_flag_store_release(&astat[rid], 2u);
         }
-        wave_lds_fence();
-        if (sv == 1u && !released) __hip_atomic_store(&astat[rid], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
         uint32_t fin = 1u;
 #pragma unroll
@@ -1505,11 +1504,12 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
   uint32_t u_drawn = 0;
   uint32_t partner = 0;
   // Bounds (never reached by a correct run): an iteration that moves or finalizes some env advances one of the
-  // wave's 2 * kE * T phases, so there are at most 2 * kE * T of them; iterations in which every unfinished env
-  // waits on a search last as long as that search (at most 100 attempts), so 2^24 of them (seconds) means a
-  // lost record -- the wave then ends instead of hanging the GPU.
-  const int64_t cap = 2 * (int64_t)kE * T + 4096;
-  int64_t work_it = 0, idle_it = 0;
+  // wave's 2 * kE * T phases, so there are at most 2 * kE * T of them; a run of iterations in which every
+  // unfinished env waits on a search lasts as long as that search (at most 100 attempts), so 2^24 of them in a
+  // row (seconds) means a lost record.  Either cap ends the wave instead of hanging the GPU, and the wave then
+  // raises the handle's status word (kStatusAsyncCap): the host fails the next call with BB_ERR_DEVICE.
+  const int64_t cap = r.work_cap > 0 ? r.work_cap : 2 * (int64_t)kE * T + 4096;
+  int64_t work_it = 0, idle_it = 0;  // idle_it: the current run of all-blocked iterations
 #if BB_ASYNC_DIAG  // iterations, cycles, blocked env-iterations, iterations that moved no env
   uint64_t dit = 0, dblk = 0, didle = 0;
   const uint64_t dt0 = __builtin_amdgcn_s_memtime();
@@ -1532,8 +1532,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     // 1. answered searches: the stream after the accepted attempt and its hand
     auto poll = [&]() {
     if (primary && ph == 1) {
-      if (__hip_atomic_load(&astat[rid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u) {
-        wave_lds_fence();
+      if (lds_flag_load_acquire(&astat[rid]) == 2u) {
         const ARec& R = arec[rid];
         s.rng.hi = R.hi;
         s.rng.lo = R.lo;
@@ -1541,7 +1540,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         const uint32_t hi = R.has_ids;
         s.rng.has = hi & 1u;
         s.hand = (hi >> 1) | ((hi & 1u) << 22);
-        astat[rid] = 0u;
+        __hip_atomic_store(&astat[rid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ph = 2;
       }
     }
@@ -1614,8 +1613,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
           R.has_ids = s.rng.has ? 1u : 0u;
           R.inc_hi = s.rng.inc_hi;
           R.inc_lo = s.rng.inc_lo;
-          wave_lds_fence();
-          __hip_atomic_store(&astat[rid], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          lds_flag_store_release(&astat[rid], 1u);
           ph = 1;
         }
       } else {
@@ -1690,9 +1688,13 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
       __builtin_amdgcn_s_sleep(1);
     } else {
       ++work_it;
+      idle_it = 0;
     }
   }
   __builtin_amdgcn_s_setprio(0);
+  // left through a cap with envs short of T steps: this launch's outputs and final state are incomplete
+  if (__ballot(primary && st < T) && lane == 0)
+    __hip_atomic_store(e.status, kStatusAsyncCap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #if BB_ASYNC_DIAG
   if (a.dbg_out && lane == 0) {
     uint64_t* o = a.dbg_out + 4 * ((size_t)blockIdx.x * kAEW + wv);
@@ -1722,9 +1724,9 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     }
     if (r.next_action) r.next_action[i] = act;
   }
-  // every request this wave posted has been answered (an env is posted only while st < T)
-  wave_lds_fence();
-  if (lane == 0) __hip_atomic_store(&afin[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // every request this wave posted has been answered (an env is posted only while st < T), unless a cap
+  // ended the wave: the search waves then finish what they claimed and leave
+  if (lane == 0) lds_flag_store_release(&afin[wv], 1u);
 }
 
 // ---------------------------------------------------------------------------

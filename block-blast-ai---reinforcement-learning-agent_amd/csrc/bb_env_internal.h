@@ -34,7 +34,11 @@ struct EnvDev {
   uint8_t* has_seed;    // seed_value is not None -> re-seed on reset
   uint8_t* pend;        // parked by step_kernel, finished by escalate_kernel
   uint64_t* pscratch;   // parked env's unfinished attempt + move summary
+  uint32_t* status;     // device-side failure word (host-pinned, device-mapped); 0 = ok, see kStatus*
 };
+
+// Device-side failure codes written to EnvDev::status (the host turns them into BB_ERR_DEVICE).
+constexpr uint32_t kStatusAsyncCap = 1u;  // rollout_async_kernel: an env wave left through an iteration cap
 
 struct StepArgs {
   bb_reward_cfg cfg;
@@ -77,6 +81,8 @@ struct RollArgs {
   double* reward_f64;           // [T][N] optional: the fp64 reward
   int64_t* final_score;         // [T][N] optional: written where the env terminated at step t (pre-reset score)
   int32_t* final_moves;         // [T][N] optional: likewise its moves
+  int64_t work_cap;             // rollout_async_kernel: working iterations per env wave (0: 2 * 64 * T + 4096;
+                                // smaller only to test the cap's error path, BB_DEBUG_ASYNC_CAP)
 };
 
 hipError_t launch_reset(const EnvDev& e, const PieceRow* rows, const uint8_t* d, const uint8_t* sel, hipStream_t s);

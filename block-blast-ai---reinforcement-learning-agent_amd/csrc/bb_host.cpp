@@ -473,6 +473,12 @@ int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions, const bb_ro
   return BB_OK;
 }
 
+// every call runs to completion on the calling thread, and no loop here is bounded by a cap: nothing to report
+int bb_sync(bb_env* env, void* stream) {
+  (void)stream;
+  return env ? BB_OK : BB_ERR_ARG;
+}
+
 // engine.py:478-507 / wrappers.py:118-126: board plane + unused pieces' shapes at
 // the origin, f32 [N][4][8][8]; masks as int8 / f32 [N][192] and bits [N][3]
 int bb_obs(bb_env* env, float* d_x, int8_t* d_mask_i8, float* d_mask_f32, uint64_t* d_mask_bits, void* stream) {

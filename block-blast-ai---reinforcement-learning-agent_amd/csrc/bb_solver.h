@@ -485,6 +485,19 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Hand-off flags between the waves of one workgroup (rollout_async_kernel's records): the payload travels
+// through LDS only, so the release / acquire fences order LDS accesses alone (workgroup scope, local
+// address space: one s_waitcnt lgkmcnt(0), no wait on the wave's outstanding global stores).
+__device__ __forceinline__ void lds_flag_store_release(uint32_t* f, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_flag_load_acquire(uint32_t* f) {
+  const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  return v;
+}
+
 // Exact level 2 of the undecided slots, flattened over the wave: the
 // reference DFS's own leaf tests (engine.py:196-224 _can_place_remaining),
 // one per lane -- for every undecided slot, every anchor q of b (then c must

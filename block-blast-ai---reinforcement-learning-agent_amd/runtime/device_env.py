@@ -214,6 +214,11 @@ class DeviceEnvBatch:
         L.check(self.lib.bb_rollout(self.handle, int(steps), _ptr(actions), C.byref(o), _stream(self.device)),
                 "bb_rollout", self.handle, self.lib)
 
+    def sync(self) -> None:
+        """Wait for this handle's launches on the current stream and raise BBNativeError if a kernel reported
+        a device-side failure (bb_sync; e.g. a rollout wave that hit its iteration cap)."""
+        L.check(self.lib.bb_sync(self.handle, _stream(self.device)), "bb_sync", self.handle, self.lib)
+
     def obs(self, x=None, mask_i8=None, mask_f32=None, mask_bits=None) -> None:
         L.check(
             self.lib.bb_obs(self.handle, _ptr(x), _ptr(mask_i8), _ptr(mask_f32), _ptr(mask_bits),

@@ -60,7 +60,7 @@ class Info(C.Structure):
     ]
 
 
-ABI_VERSION = 2  # include/bbvec.h BB_ABI_VERSION
+ABI_VERSION = 3  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -128,6 +128,7 @@ SIGNATURES = {
     "bb_reset": (C.c_int, [_P, _P, _P]),
     "bb_step": (C.c_int, [_P, _P, C.POINTER(StepOut), _P]),
     "bb_rollout": (C.c_int, [_P, _I32, _P, C.POINTER(RolloutOut), _P]),
+    "bb_sync": (C.c_int, [_P, _P]),
     "bb_obs": (C.c_int, [_P, _P, _P, _P, _P, _P]),
     "bb_device_ptrs": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P)]),
     "bb_snapshot": (C.c_int, [_P, _P, _P, _P, _P]),
@@ -172,7 +173,7 @@ SIGNATURES = {
 
 # the env entry points, which the host backend (libbbvec_host.so) exports too
 HOST_SYMBOLS = ("bb_abi_version", "bb_create", "bb_destroy", "bb_last_error", "bb_num_envs", "bb_pcg64_seed",
-                "bb_seed", "bb_reset", "bb_step", "bb_rollout", "bb_obs", "bb_device_ptrs", "bb_snapshot",
+                "bb_seed", "bb_reset", "bb_step", "bb_rollout", "bb_sync", "bb_obs", "bb_device_ptrs", "bb_snapshot",
                 "bb_get_state", "bb_set_state", "bb_random_actions")
 
 _lib = None
@@ -198,9 +199,7 @@ def load(path: str | None = None):
             fn.restype = res
             fn.argtypes = args
         v = lib.bb_abi_version()
-        # an A/B arm built from an earlier revision (BBVEC_LIB, tools/build_prev.sh) may be ABI 1: version 2
-        # only appended bb_step_out fields, which such a library never reads
-        if v != ABI_VERSION and not (os.environ.get("BBVEC_LIB") and v == 1):
+        if v != ABI_VERSION:
             raise BBNativeError(f"libbbvec ABI version mismatch ({v}, expected {ABI_VERSION})")
         if path is None:
             _lib = lib

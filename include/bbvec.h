@@ -32,12 +32,13 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 2  /* 2: bb_step_out.final_score / final_moves */
+#define BB_ABI_VERSION 3  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
 #define BB_ERR_HIP (-2)
 #define BB_ERR_STATE (-3)
+#define BB_ERR_DEVICE (-4) /* a kernel reported a failure through the handle's status word */
 
 #define BB_NUM_PIECES 37
 #define BB_ACTIONS 192
@@ -183,6 +184,18 @@ typedef struct bb_rollout_out {
 
 int bb_rollout(bb_env* env, int32_t steps, const int32_t* d_actions,
                const bb_rollout_out* out, void* stream);
+
+/* Device-side failures.  The rollout kernel bounds its own iterations so that
+ * a logic error can never hang the GPU; if a bound is ever hit it writes the
+ * handle's status word instead of failing silently.  Every later bb_step /
+ * bb_rollout / bb_get_state / masked bb_reset then returns BB_ERR_DEVICE
+ * (bb_last_error says which kernel and why) until a full bb_reset (d_env_mask
+ * NULL).  Launches are asynchronous, so the check at the next call sees only
+ * the launches that have finished by then; bb_sync waits for every launch on
+ * `stream` and reports their status (BB_OK or BB_ERR_DEVICE / BB_ERR_HIP).
+ * The reference has no device side; this replaces the exceptions its Python
+ * step loop would raise (wrappers.py:75-116). */
+int bb_sync(bb_env* env, void* stream);
 
 /* Observation expansion (engine.py:478-507, block_blast_env.py:134-146,
  * wrappers.py:118-126).  Any output may be NULL:
