@@ -34,6 +34,12 @@ constexpr uint64_t kCenter = 0x00003C3C3C3C0000ull;  // rows 2-5 x cols 2-5 (boa
 //             is (the hardware reads bits 5:0).  anchors_of costs 6 shifts
 //             for every piece instead of one per cell (9 for SQUARE_3x3 =
 //             {0,1,2} + {0,8} + {0,8}).
+#ifndef BB_ROW_PAD
+// bytes of padding per PieceRow: a 72-byte stride (an odd number of 8-byte words) spreads the lanes'
+// per-piece LDS reads over every bank (64-byte rows: 5.2x the bank-conflict cycles and -4% on the rollout;
+// 80 / 88 / 104 bytes: -1.3% / -0.4% / +0.1%; profiles/r04/p2_*)
+#define BB_ROW_PAD 8
+#endif
 struct PieceRow {
   uint64_t shape;
   uint64_t anchors;
@@ -41,6 +47,9 @@ struct PieceRow {
   uint64_t ym_lo;
   uint64_t ym_hi;
   uint32_t sh[6];
+#if BB_ROW_PAD
+  uint8_t pad[BB_ROW_PAD];
+#endif
 };
 
 __host__ __device__ inline uint32_t ncells_of(const PieceRow& p) { return (p.sh[5] >> 8) & 0xFFu; }
@@ -48,8 +57,14 @@ __host__ __device__ inline uint32_t ncells_of(const PieceRow& p) { return (p.sh[
 // PCG64 jump-ahead table row c: A^c and S_c = sum_{i<c} A^i (mod 2^128), so
 // the state after c steps is A^c * s + inc * S_c (built on the host).
 constexpr int kJumpMax = 64;
+#ifndef BB_JUMP_PAD
+#define BB_JUMP_PAD 0  // bytes of padding per JumpRow
+#endif
 struct JumpRow {
   uint64_t a_lo, a_hi, s_lo, s_hi;
+#if BB_JUMP_PAD
+  uint8_t pad[BB_JUMP_PAD];
+#endif
 };
 
 // Board.can_place over all anchors at once (board.py:71-93 x engine.py:364-380):

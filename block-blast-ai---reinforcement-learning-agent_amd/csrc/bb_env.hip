@@ -56,14 +56,14 @@ constexpr int kDPad = (kPieces * kPieces + 15) / 16 * 16;  // |D| table padded t
 
 struct alignas(16) Tables {
   PieceRow row[kPieces];
-  uint8_t d[kDPad];
+  alignas(16) uint8_t d[kDPad];
 };
-static_assert(sizeof(PieceRow) % 16 == 0, "PieceRow staged as 16-byte vectors");
+static_assert(sizeof(PieceRow) % 8 == 0, "PieceRow staged as 8-byte vectors");
 
-// Global -> LDS copy of the piece rows and the |D| table (and, for the
-// kernels that run hand searches, the PCG64 jump-ahead table) as 16-byte
-// vectors: every load of a thread is issued before its first LDS store, so
-// the staging costs one memory latency (byte-wise copying cost ~22 serial
+// Global -> LDS copy of the piece rows (8-byte vectors: a row stride of an odd number of 8-byte words
+// spreads the lanes' per-piece reads over every LDS bank) and of the |D| table (and, for the kernels that
+// run hand searches, the PCG64 jump-ahead table) as 16-byte vectors: every load of a thread is issued
+// before its first LDS store, so the staging costs one memory latency (byte-wise copying cost ~22 serial
 // ones).  The device buffers are padded (slab carving rounds to 256 bytes).
 constexpr int kJumpVec = (kJumpMax + 1) * (int)sizeof(JumpRow) / 16;
 static_assert(sizeof(JumpRow) % 16 == 0, "JumpRow staged as 16-byte vectors");
@@ -71,30 +71,40 @@ static_assert(sizeof(JumpRow) % 16 == 0, "JumpRow staged as 16-byte vectors");
 template <bool kWithJump = false>
 __device__ __forceinline__ void stage_tables(Tables& t, const PieceRow* g_rows, const uint8_t* g_d,
                                              JumpRow* jt = nullptr, const JumpRow* g_jump = nullptr) {
-  constexpr int kRowVec = kPieces * (int)sizeof(PieceRow) / 16;
-  constexpr int kTabVec = kRowVec + kDPad / 16;
+  constexpr int kRow8 = kPieces * (int)sizeof(PieceRow) / 8;
+  constexpr int kTabVec = kDPad / 16;
   constexpr int kTot = kTabVec + (kWithJump ? kJumpVec : 0);
   constexpr int kPer = (kTot + 63) / 64;
+  constexpr int kPer8 = (kRow8 + 63) / 64;
   const int tid = threadIdx.x;
   const int nthr = (int)blockDim.x;
   // one source / destination address per vector (a single select each), so the
   // staged values stay in registers (a pointer select per load put them in scratch)
+  uint2 w[kPer8];
+#pragma unroll
+  for (int k = 0; k < kPer8; ++k) {
+    const int idx = tid + k * nthr;
+    w[k] = reinterpret_cast<const uint2*>(g_rows)[idx < kRow8 ? idx : 0];
+  }
   uint4 v[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int idx = tid + k * nthr;
     const int j = idx < kTot ? idx : 0;
-    const char* src = j < kRowVec ? reinterpret_cast<const char*>(g_rows) + 16 * j
-                    : j < kTabVec ? reinterpret_cast<const char*>(g_d) + 16 * (j - kRowVec)
+    const char* src = j < kTabVec ? reinterpret_cast<const char*>(g_d) + 16 * j
                                   : reinterpret_cast<const char*>(g_jump) + 16 * (j - kTabVec);
     v[k] = *reinterpret_cast<const uint4*>(src);
+  }
+#pragma unroll
+  for (int k = 0; k < kPer8; ++k) {
+    const int idx = tid + k * nthr;
+    if (idx < kRow8) reinterpret_cast<uint2*>(t.row)[idx] = w[k];
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int idx = tid + k * nthr;
     if (idx < kTot) {
-      char* dst = idx < kRowVec ? reinterpret_cast<char*>(t.row) + 16 * idx
-                : idx < kTabVec ? reinterpret_cast<char*>(t.d) + 16 * (idx - kRowVec)
+      char* dst = idx < kTabVec ? reinterpret_cast<char*>(t.d) + 16 * idx
                                 : reinterpret_cast<char*>(jt) + 16 * (idx - kTabVec);
       *reinterpret_cast<uint4*>(dst) = v[k];
     }
@@ -1302,11 +1312,13 @@ constexpr int kAE = BB_ASYNC_ENVS;
 static_assert(kAE == 32 || kAE == 64, "async env waves: 32 or 64 envs");
 constexpr int kAEnvs = kAE * kAEW;  // envs per workgroup
 
-// One posted env: the board and stream state on the way in; stream state and hand ids on the way back.
-struct ARec {
-  uint64_t B, hi, lo;
-  uint32_t buf, has_ids;  // has | ids << 1 on the way back
-  uint64_t inc_hi, inc_lo;  // BB_ASYNC_POOL: the stream increment (any search wave may take the env)
+// The posted envs of a workgroup, one record per env, as structure of arrays (the lanes of a wave touch
+// consecutive records: conflict-free LDS access).  In: board and stream state; back: stream state and the
+// hand ids (has | ids << 1).
+struct ARecs {
+  uint64_t B[kAEnvs], hi[kAEnvs], lo[kAEnvs];
+  uint64_t inc_hi[kAEnvs], inc_lo[kAEnvs];  // the stream increment (any search wave may take the env)
+  uint32_t buf[kAEnvs], has_ids[kAEnvs];
 };
 
 __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, const PieceRow* g_rows,
@@ -1316,7 +1328,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
   __shared__ Tables t;
   __shared__ uint32_t scratch[kABlock];  // 64 words per wave (the search waves' slow_phase_wave)
   __shared__ JumpRow jt[kJumpMax + 1];
-  __shared__ ARec arec[kAEnvs];
+  __shared__ ARecs arec;
   __shared__ uint32_t astat[kAEnvs];  // 0 idle, 1 posted, 2 answered
   __shared__ uint32_t afin[kAEW];
   __shared__ uint32_t wave_simd[kAEW + kASW];
@@ -1350,8 +1362,12 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     int rid = pool ? lane : sw * kOwn + lane;
     const bool mine = lane < kOwn;
     uint64_t B = 0ull;
-#if BB_ASYNC_DIAG  // diagnostics (BB_DEBUG_MODE=16): calls, envs served, search cycles, polls
+#if BB_ASYNC_DIAG  // diagnostics (BB_DEBUG_MODE=16): calls, envs served, search cycles, polls, phase cycles, rounds
     uint64_t dcalls = 0, denvs = 0, dcyc = 0, dpolls = 0;
+    uint64_t dprof[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t* const dprof_p = dprof;
+#else
+    uint64_t* const dprof_p = nullptr;
 #endif
 #pragma unroll 1
     for (;;) {
@@ -1378,14 +1394,13 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         // acquire: the claimed records' fields were written before their poster's release of status 1
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         if (sv == 1u) {
-          const ARec& R = arec[rid];
-          B = R.B;
-          rng.hi = R.hi;
-          rng.lo = R.lo;
-          rng.buf = R.buf;
-          rng.has = R.has_ids & 1u;
-          rng.inc_hi = R.inc_hi;
-          rng.inc_lo = R.inc_lo;
+          B = arec.B[rid];
+          rng.hi = arec.hi[rid];
+          rng.lo = arec.lo[rid];
+          rng.buf = arec.buf[rid];
+          rng.has = arec.has_ids[rid] & 1u;
+          rng.inc_hi = arec.inc_hi[rid];
+          rng.inc_lo = arec.inc_lo[rid];
         }
         __builtin_amdgcn_s_setprio(BB_ASYNC_SPRIO);
         uint32_t ids = 0;
@@ -1397,17 +1412,16 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         // envs decided in an earlier round of the call go back to their env waves at once
         auto release = [&](bool d) {
           if (d && sv == 1u) {
-            ARec& R = arec[rid];
-            R.hi = rng.hi;
-            R.lo = rng.lo;
-            R.buf = rng.buf;
-            R.has_ids = (rng.has ? 1u : 0u) | (ids << 1);
+            arec.hi[rid] = rng.hi;
+            arec.lo[rid] = rng.lo;
+            arec.buf[rid] = rng.buf;
+            arec.has_ids[rid] = (rng.has ? 1u : 0u) | (ids << 1);
             lds_flag_store_release(&astat[rid], 2u);
             released = true;
           }
         };
         gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
-                                                     a.pack_next, lds, nullptr, 0, release);
+                                                     a.pack_next, lds, dprof_p, 0, release);
 #else
         gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
                                                      a.pack_next, lds);
@@ -1419,11 +1433,10 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
 #endif
         __builtin_amdgcn_s_setprio(0);
         if (sv == 1u && !released) {
-          ARec& R = arec[rid];
-          R.hi = rng.hi;
-          R.lo = rng.lo;
-          R.buf = rng.buf;
-          R.has_ids = (rng.has ? 1u : 0u) | (ids << 1);
+          arec.hi[rid] = rng.hi;
+          arec.lo[rid] = rng.lo;
+          arec.buf[rid] = rng.buf;
+          arec.has_ids[rid] = (rng.has ? 1u : 0u) | (ids << 1);
           lds_flag_store_release(&astat[rid], 2u);
         }
       } else {
@@ -1440,11 +1453,12 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     }
 #if BB_ASYNC_DIAG
     if (a.dbg_out && lane == 0) {
-      uint64_t* o = a.dbg_out + 4 * ((size_t)(e.n + 31) / 32 + (size_t)blockIdx.x * kASW + sw);
+      uint64_t* o = a.dbg_out + 4 * ((size_t)(e.n + 31) / 32) + 12 * ((size_t)blockIdx.x * kASW + sw);
       o[0] = dcalls;
       o[1] = denvs;
       o[2] = dcyc;
       o[3] = dpolls;
+      for (int q = 0; q < 6; ++q) o[4 + q] = dprof[q];
     }
 #endif
     return;
@@ -1510,14 +1524,15 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
   // raises the handle's status word (kStatusAsyncCap): the host fails the next call with BB_ERR_DEVICE.
   const int64_t cap = r.work_cap > 0 ? r.work_cap : 2 * (int64_t)kE * T + 4096;
   int64_t work_it = 0, idle_it = 0;  // idle_it: the current run of all-blocked iterations
-#if BB_ASYNC_DIAG  // iterations, cycles, blocked env-iterations, iterations that moved no env
-  uint64_t dit = 0, dblk = 0, didle = 0;
+#if BB_ASYNC_DIAG  // iterations, cycles, blocked env-iterations, iterations that moved no env | their cycles << 32
+  uint64_t dit = 0, dblk = 0, didle = 0, didle_cyc = 0;
   const uint64_t dt0 = __builtin_amdgcn_s_memtime();
 #endif
 #pragma unroll 1
   for (int it = 0; work_it < cap && idle_it < (1 << 24); ++it) {
     if (!__ballot(primary && st < T)) break;
 #if BB_ASYNC_DIAG
+    const uint64_t dti = __builtin_amdgcn_s_memtime();
     dit += 1;
     dblk += (uint64_t)__popcll(__ballot(primary && ph == 1));
     didle += __ballot(primary && ph != 1 && st < T) ? 0u : 1u;
@@ -1533,11 +1548,10 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     auto poll = [&]() {
     if (primary && ph == 1) {
       if (lds_flag_load_acquire(&astat[rid]) == 2u) {
-        const ARec& R = arec[rid];
-        s.rng.hi = R.hi;
-        s.rng.lo = R.lo;
-        s.rng.buf = R.buf;
-        const uint32_t hi = R.has_ids;
+        s.rng.hi = arec.hi[rid];
+        s.rng.lo = arec.lo[rid];
+        s.rng.buf = arec.buf[rid];
+        const uint32_t hi = arec.has_ids[rid];
         s.rng.has = hi & 1u;
         s.hand = (hi >> 1) | ((hi & 1u) << 22);
         __hip_atomic_store(&astat[rid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1605,14 +1619,13 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
         if (accepted) {
           ph = 2;
         } else {  // post the env: post-move board, stream rolled back to attempt 1
-          ARec& R = arec[rid];
-          R.B = s.B;
-          R.hi = s.rng.hi;
-          R.lo = s.rng.lo;
-          R.buf = s.rng.buf;
-          R.has_ids = s.rng.has ? 1u : 0u;
-          R.inc_hi = s.rng.inc_hi;
-          R.inc_lo = s.rng.inc_lo;
+          arec.B[rid] = s.B;
+          arec.hi[rid] = s.rng.hi;
+          arec.lo[rid] = s.rng.lo;
+          arec.buf[rid] = s.rng.buf;
+          arec.has_ids[rid] = s.rng.has ? 1u : 0u;
+          arec.inc_hi[rid] = s.rng.inc_hi;
+          arec.inc_lo[rid] = s.rng.inc_lo;
           lds_flag_store_release(&astat[rid], 1u);
           ph = 1;
         }
@@ -1686,6 +1699,9 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     if (!__ballot(mv || fin)) {  // every env blocked: leave the SIMD to the searches
       ++idle_it;
       __builtin_amdgcn_s_sleep(1);
+#if BB_ASYNC_DIAG
+      didle_cyc += __builtin_amdgcn_s_memtime() - dti;
+#endif
     } else {
       ++work_it;
       idle_it = 0;
@@ -1701,7 +1717,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     o[0] = dit;
     o[1] = __builtin_amdgcn_s_memtime() - dt0;
     o[2] = dblk;
-    o[3] = didle;
+    o[3] = didle | (didle_cyc << 32);
   }
 #endif
   if (primary) {

@@ -47,7 +47,9 @@ def main():
         env.lib.bb_debug_counters(env.handle, buf.ctypes.data_as(C.c_void_p))
         flat = buf.reshape(-1)
         we = flat[: 4 * nwe].reshape(-1, 4).astype(np.float64)
-        ws = flat[4 * soff: 4 * (soff + nws)].reshape(-1, 4).astype(np.float64)
+        wsx = flat[4 * soff: 4 * soff + 12 * nws].reshape(-1, 12).astype(np.float64)
+        ws = wsx[:, :4]
+        ph = wsx[:, 4:10].sum(axis=0) / max(ws[:, 0].sum(), 1)  # gen_hands_multi phase cycles per call
         out.append({
             "call": call, "T": T,
             "env_iters_per_step": round(we[:, 0].mean() / T, 4),
@@ -56,12 +58,15 @@ def main():
             "env_wave_cyc_mean": round(we[:, 1].mean(), 0),
             "env_wave_cyc_max": int(we[:, 1].max()),
             "blocked_envs_per_iter_per_wave": round(we[:, 2].sum() / we[:, 0].sum(), 3),
-            "idle_iters_per_wave": round(we[:, 3].mean(), 2),
+            "idle_iters_per_wave": round((flat[: 4 * nwe].reshape(-1, 4)[:, 3] & 0xFFFFFFFF).astype(np.float64).mean(), 2),
+            "idle_cyc_frac": round((flat[: 4 * nwe].reshape(-1, 4)[:, 3] >> 32).astype(np.float64).sum() / we[:, 1].sum(), 4),
             "search_calls_per_wave": round(ws[:, 0].mean(), 1),
             "envs_per_call": round(ws[:, 1].sum() / max(ws[:, 0].sum(), 1), 2),
             "cyc_per_call": round(ws[:, 2].sum() / max(ws[:, 0].sum(), 1), 0),
             "search_busy_frac": round(ws[:, 2].sum() / (we[:, 1].mean() * len(ws)), 3),
             "polls_per_wave": round(ws[:, 3].mean(), 1),
+            "call_phase_cyc": {k: round(float(v), 0) for k, v in zip(
+                ("setup_draws", "anchors_pack", "pass_quick", "pass_exact", "pass_overhead", "resolve"), ph)},
         })
         buf[:] = 0
         env.lib.bb_debug_counters  # counters are overwritten by every launch

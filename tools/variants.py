@@ -67,6 +67,24 @@ VARIANTS = {
     "adiag": ["-DBB_ASYNC_DIAG=1"],
     "adiagp": ["-DBB_ASYNC_DIAG=1", "-DBB_ASYNC_POOL=1"],
     "adiag2": ["-DBB_ASYNC_DIAG=1", "-DBB_ASYNC_SPRIO=2"],
+    # env waves: an env moves only while it is < W steps ahead of its wave's slowest env (output-row window)
+    "aw4": ["-DBB_ASYNC_WINDOW=4"],
+    "aw8": ["-DBB_ASYNC_WINDOW=8"],
+    "aw12": ["-DBB_ASYNC_WINDOW=12"],
+    "aw16": ["-DBB_ASYNC_WINDOW=16"],
+    "aw24": ["-DBB_ASYNC_WINDOW=24"],
+    # env waves: output rows [lo, lo + R) staged in LDS and written out as whole lines (BB_ASYNC_RING)
+    "ar8": ["-DBB_ASYNC_RING=8"],
+    "ar12": ["-DBB_ASYNC_RING=12"],
+    "ar16": ["-DBB_ASYNC_RING=16"],
+    "adiagr16": ["-DBB_ASYNC_DIAG=1", "-DBB_ASYNC_RING=16"],
+    # LDS bank spread of the per-lane table reads: PieceRow 64 -> 80 bytes, JumpRow 32 -> 48 bytes
+    "rp16": ["-DBB_ROW_PAD=16"],
+    "jp16": ["-DBB_JUMP_PAD=16"],
+    "rjp16": ["-DBB_ROW_PAD=16", "-DBB_JUMP_PAD=16"],
+    "rp8": ["-DBB_ROW_PAD=8"],
+    "rp24": ["-DBB_ROW_PAD=24"],
+    "rp40": ["-DBB_ROW_PAD=40"],
     # rollout kernel workgroup shape (waves per workgroup; SIMD partners share LDS progress words at 512)
     "rblk64": ["-DBB_ROLL_BLOCK=64"],
     "rblk256": ["-DBB_ROLL_BLOCK=256"],
