@@ -299,6 +299,16 @@ class PPOAgent(BaseAgent):
         self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if sample_seed is None else int(sample_seed)
         self.sample_step = 0
         self._flat_grad = None
+        # data parallelism (world > 1): the flat gradient buffer is all-reduced in buckets of about this many
+        # floats, each launched asynchronously as soon as backward has accumulated its last gradient, so the
+        # RCCL traffic overlaps the rest of the backward pass; "capture" also captures those collectives
+        # inside the optimizer step's HIP graph (one graph per step instead of two around an eager
+        # all-reduce; needs the nccl = RCCL backend, opt-in: unmeasured on an 8-GPU node)
+        self.dp_bucket_floats = 1 << 20
+        self.dp_overlap = "graph-split"  # or "capture"
+        self._dp_hooks = None
+        self._dp_hooks_on = True  # off while a graph without collectives is captured
+        self._dp_works: List[Any] = []
         # bumped whenever parameter storage, layout or precision changes: captured graphs of the
         # optimizer step (here) and of the rollout (training.trainer.DeviceRollout) are then stale
         self.graph_epoch = 0
@@ -337,6 +347,7 @@ class PPOAgent(BaseAgent):
         self._graphs = {}
         self.graph_epoch += 1
         self._flat_grad = None  # gradient views must follow the parameters' strides
+        self._remove_dp_hooks()
 
     def _raw(self, x: torch.Tensor):
         if self.channels_last and x.is_cuda:
@@ -415,8 +426,9 @@ class PPOAgent(BaseAgent):
     def _grad_buffer(self) -> torch.Tensor:
         """Flat fp32 gradient buffer for data-parallel runs; every parameter's
         .grad is a view into it (same strides as the parameter, 256-byte
-        aligned so the accumulating adds stay vectorised), so one all-reduce
-        covers the whole model (5,290,113 floats plus alignment padding)."""
+        aligned so the accumulating adds stay vectorised), so the all-reduce
+        covers the whole model (5,290,113 floats plus alignment padding) in a
+        few contiguous buckets (_dp_buckets)."""
         if self._flat_grad is None:
             params = [p for p in self.network.parameters() if p.requires_grad]
             offs, n = [], 0
@@ -426,7 +438,76 @@ class PPOAgent(BaseAgent):
             self._flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
             for p, off in zip(params, offs):
                 p.grad = torch.as_strided(self._flat_grad, p.size(), p.stride(), off)
+            self._flat_layout = [(p, off, -(-p.numel() // 64) * 64) for p, off in zip(params, offs)]
+            self._remove_dp_hooks()  # the buckets are ranges of this buffer
         return self._flat_grad
+
+    def _remove_dp_hooks(self) -> None:
+        if self._dp_hooks is not None:
+            for h in self._dp_hooks[0]:
+                h.remove()
+        self._dp_hooks = None
+
+    def _dp_buckets(self):
+        """Post-accumulate-grad hooks that all-reduce the flat gradient buffer in contiguous buckets.  Backward
+        produces the gradients roughly in reverse parameter order, so the buckets are taken from the end of the
+        buffer; a bucket's all-reduce is issued (async_op) once all of its parameters have accumulated, and
+        ``_dp_finish`` waits for them (a bucket that never completed is issued there)."""
+        flat = self._grad_buffer()
+        if self._dp_hooks is not None:
+            return self._dp_hooks
+        layout = self._flat_layout
+        buckets, cur, size = [], [], 0
+        for p, off, n in reversed(layout):
+            cur.append((p, off, n))
+            size += n
+            if size >= self.dp_bucket_floats:
+                buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            buckets.append(cur)
+        state = []  # per bucket: [lo, hi, remaining, total, launched]
+        owner = {}
+        for b, items in enumerate(buckets):
+            lo = min(off for _, off, _ in items)
+            hi = max(off + n for _, off, n in items)
+            state.append([lo, hi, len(items), len(items), False])
+            for p, _, _ in items:
+                owner[p] = b
+
+        def make_hook(b):
+            def hook(_p):
+                if not self._dp_hooks_on:
+                    return
+                st = state[b]
+                st[2] -= 1
+                if st[2] == 0 and not st[4]:
+                    st[4] = True
+                    self._dp_works.append(dist.all_reduce(flat[st[0]:st[1]], async_op=True))
+            return hook
+
+        handles = [p.register_post_accumulate_grad_hook(make_hook(owner[p])) for p, _, _ in layout]
+        self._dp_hooks = (handles, state)
+        return self._dp_hooks
+
+    def _dp_arm(self) -> None:
+        """Before a backward pass: every bucket waits for all of its gradients again."""
+        for st in self._dp_buckets()[1]:
+            st[2], st[4] = st[3], False
+        self._dp_works = []
+
+    def _dp_finish(self, world: int) -> None:
+        """After backward: issue the buckets whose hooks did not all fire, wait for every bucket's all-reduce
+        (the current stream waits on RCCL's; the host does not block), then average."""
+        flat = self._flat_grad
+        for st in self._dp_hooks[1]:
+            if not st[4]:
+                st[4] = True
+                self._dp_works.append(dist.all_reduce(flat[st[0]:st[1]], async_op=True))
+        for w in self._dp_works:
+            w.wait()
+        self._dp_works = []
+        flat.div_(world)
 
     def _minibatch_loss(self, x, masks, actions, old_log_probs, advantages, returns):
         cfg = self.config
@@ -438,14 +519,15 @@ class PPOAgent(BaseAgent):
 
     def _optimizer_step(self, loss: torch.Tensor) -> None:
         world = _world()
-        if world > 1:  # one all-reduce (average) of the flat gradient buffer per optimizer step
+        if world > 1:  # all-reduce (average) of the flat gradient buffer, bucketed and overlapped with backward
             flat = self._grad_buffer()
             flat.zero_()
+            self._dp_arm()
             loss.backward()
-            dist.all_reduce(flat)
-            flat.div_(world)
+            self._dp_finish(world)
         else:  # autograd hands its gradient tensors over: no zero fill, no accumulating adds
             self._flat_grad = None
+            self._remove_dp_hooks()
             for p in self.network.parameters():
                 p.grad = None
             loss.backward()
@@ -517,13 +599,14 @@ class PPOAgent(BaseAgent):
         ent = self._graphs.get(key)
         if ent is None:
             ent = self._graphs[key] = self._capture_step(inputs)
-        graphs, static_in, static_stats = ent
+        graphs, static_in, static_stats, flat = ent
         for dst, src in zip(static_in, inputs):
             if dst.data_ptr() != src.data_ptr():  # minibatch_inputs() buffers are the inputs already
                 dst.copy_(src)
         graphs[0].replay()
-        if len(graphs) > 1:  # one all-reduce of the flat fp32 gradient buffer (RCCL over xGMI), then the step
-            dist.all_reduce(self._flat_grad)
+        if len(graphs) > 1:  # the all-reduce of the flat fp32 gradient buffer (RCCL over xGMI), then the step
+            work = dist.all_reduce(flat, async_op=True)  # graph B waits on it on the device, the host goes on
+            work.wait()
             graphs[1].replay()
         return static_stats
 
@@ -566,19 +649,27 @@ class PPOAgent(BaseAgent):
             # by the capture's backward and flagged as a stream mismatch
             del loss
         graphs = [torch.cuda.CUDAGraph()]
-        if world == 1:
+        flat = self._flat_grad
+        if world == 1 or self.dp_overlap == "capture":
+            # one graph per step; data parallel: the bucketed all-reduces issued by the backward hooks are
+            # captured with it (RCCL collectives in a HIP graph)
             with torch.cuda.graph(graphs[0], stream=side):
                 loss, stats = self._minibatch_loss(*static_in)
                 self._optimizer_step(loss)
                 del loss
+            flat = self._flat_grad
         else:
             flat = self._grad_buffer()  # every .grad a view into it (made by the warm-up's eager steps)
             graphs.append(torch.cuda.CUDAGraph())
-            with torch.cuda.graph(graphs[0], stream=side):
-                flat.zero_()
-                loss, stats = self._minibatch_loss(*static_in)
-                loss.backward()
-                del loss
+            self._dp_hooks_on = False  # graph A holds no collective: the all-reduce runs between the replays
+            try:
+                with torch.cuda.graph(graphs[0], stream=side):
+                    flat.zero_()
+                    loss, stats = self._minibatch_loss(*static_in)
+                    loss.backward()
+                    del loss
+            finally:
+                self._dp_hooks_on = True
             with torch.cuda.graph(graphs[1], stream=side, pool=graphs[0].pool()):
                 flat.div_(world)
                 self._clip_and_step()
@@ -596,7 +687,7 @@ class PPOAgent(BaseAgent):
                             v.copy_(old[k])
                         else:  # fresh Adam state == zero moments at step 0
                             v.zero_()
-        return graphs, static_in, stats
+        return graphs, static_in, stats, flat
 
     def update(self, buffer, last_values, batch_size: Optional[int] = None) -> Dict[str, float]:
         """ppo.py:330-423.  Metrics are accumulated on the device and read once.
@@ -659,6 +750,7 @@ class PPOAgent(BaseAgent):
         if "config" in ckpt:
             self.config = PPOConfig.from_dict(ckpt["config"])
         self._flat_grad = None
+        self._remove_dp_hooks()
 
     def train(self) -> None:
         super().train()

@@ -57,14 +57,8 @@ __host__ __device__ inline uint32_t ncells_of(const PieceRow& p) { return (p.sh[
 // PCG64 jump-ahead table row c: A^c and S_c = sum_{i<c} A^i (mod 2^128), so
 // the state after c steps is A^c * s + inc * S_c (built on the host).
 constexpr int kJumpMax = 64;
-#ifndef BB_JUMP_PAD
-#define BB_JUMP_PAD 0  // bytes of padding per JumpRow
-#endif
 struct JumpRow {
   uint64_t a_lo, a_hi, s_lo, s_hi;
-#if BB_JUMP_PAD
-  uint8_t pad[BB_JUMP_PAD];
-#endif
 };
 
 // Board.can_place over all anchors at once (board.py:71-93 x engine.py:364-380):
@@ -278,15 +272,15 @@ __device__ __forceinline__ uint32_t policy_uniform(uint64_t seed, uint64_t idx, 
 }
 
 __device__ __forceinline__ int32_t random_policy_u(uint64_t m0, uint64_t m1, uint64_t m2, uint32_t u) {
-  uint32_t c0 = __popcll(m0), c1 = __popcll(m1), c2 = __popcll(m2);
-  uint32_t tot = c0 + c1 + c2;
-  if (tot == 0) return 0;
+  const uint32_t c0 = __popcll(m0), c1 = __popcll(m1), c2 = __popcll(m2);
+  const uint32_t tot = c0 + c1 + c2;
   uint32_t k = (uint32_t)(((uint64_t)u * tot) >> 32);
-  if (k < c0) return select_bit(m0, k);
-  k -= c0;
-  if (k < c1) return 64 + select_bit(m1, k);
-  k -= c1;
-  return 128 + select_bit(m2, k);
+  // the word holding the k-th set bit, picked by select: one select_bit, no divergent paths
+  const bool in0 = k < c0, in1 = k < c0 + c1;
+  const uint64_t w = in0 ? m0 : (in1 ? m1 : m2);
+  k -= in0 ? 0u : (in1 ? c0 : c0 + c1);
+  const int base = in0 ? 0 : (in1 ? 64 : 128);
+  return tot == 0 ? 0 : base + select_bit(w, k);
 }
 
 __device__ __forceinline__ int32_t random_policy(uint64_t m0, uint64_t m1, uint64_t m2, uint64_t seed,

@@ -19,19 +19,15 @@
 //       succeed if y at q completes a line (the clear may free room for z):
 //       those few q are checked explicitly.  Same for order z then y.
 //   level 3 is the anchors_of() != 0 test.
-// gen_hand_wave (bottom) runs the search with a whole wave per env; the
-// per-lane gen_hand_lane (budgeted) is kept for the optional in-lane mode
-// (BB_LANE_BUDGET > 0) and the parity tests that exercise it.
+// gen_hands_multi (bottom) runs the searches of several envs with a whole
+// wave; gen_hand_wave (one env per wave) serves the solver-counter diagnostic
+// mode (BB_DEBUG_MODE=2), the per-lane gen_hand_lane (budgeted) the in-lane
+// mode (BB_LANE_BUDGET > 0); the parity tests exercise all three.
 #pragma once
 #include "bb_device.h"
 
-#ifndef BB_SLOW_FLAT
-#define BB_SLOW_FLAT 1  // flattened exact level 2 (slow_phase_wave); 0: per-lane disjoint scan + line phase
-#endif
 
 namespace bb {
-
-constexpr int kUnlimited = 1 << 30;
 
 // Work-budget ticks (roughly proportional to instruction counts).
 constexpr int kTickAnchors = 4;
@@ -185,29 +181,6 @@ __device__ __forceinline__ int pair_quick(uint64_t B1, const PieceRow& pb, const
   return 2;
 }
 
-// pair_quick for the wave searches' passes: the two leaves test the second
-// piece on B1 | first piece WITHOUT the line clear.  Clearing only frees
-// cells, so a fit there is a fit after the clear: every accept is still an
-// exact success; the rarer accepts that need the clear are left (2) to the
-// exact phase (slow_phase_wave).  Saves the two clear_full of pair_quick.
-__device__ __forceinline__ int pair_quick_nc(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint32_t dbc,
-                                             uint64_t& A2, uint64_t& A3) {
-  A2 = anchors_of(pb, B1);
-  A3 = anchors_of(pc, B1);
-  if ((A2 | A3) == 0) return 0;
-  if (A2 && (uint32_t)__popcll(A3) > dbc) return 1;
-  if (A3 && (uint32_t)__popcll(A2) > dbc) return 1;
-  if (A2) {
-    const int q = __ffsll((unsigned long long)A2) - 1;
-    if (anchors_of(pc, B1 | (pb.shape << q))) return 1;
-  }
-  if (A3) {
-    const int r = __ffsll((unsigned long long)A3) - 1;
-    if (anchors_of(pb, B1 | (pc.shape << r))) return 1;
-  }
-  return 2;
-}
-
 // pair_quick without branches: 0 reject, 1 accept, 2 undecided, A2 / A3 out.
 __device__ __forceinline__ int pair_quick_bf(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint32_t dbc,
                                              uint64_t& A2, uint64_t& A3) {
@@ -221,33 +194,12 @@ __device__ __forceinline__ int pair_quick_bf(uint64_t B1, const PieceRow& pb, co
   return (A2 | A3) == 0ull ? 0 : ((dacc || leaf2 || leaf3) ? 1 : 2);
 }
 
-// Quick test of fixed level-1 slots k0 .. k0+slots-1 of the drawn hand
-// (x0, x1, x2) on B: slot k places piece k mod 3 at its lowest (k < 3) or
-// highest anchor, then pair_quick.  True on an accept (an exact success).
-__device__ __forceinline__ bool quick_slots(uint64_t B, uint32_t x0, uint32_t x1, uint32_t x2, const PieceRow* tbl,
-                                            const uint8_t* dtab, int k0, int slots) {
-#pragma unroll
-  for (int kk = 0; kk < 6; ++kk) {
-    if (kk >= slots) break;
-    const int k = k0 + kk;
-    const int f = k % 3;
-    const uint32_t fi = f == 0 ? x0 : (f == 1 ? x1 : x2);
-    const uint64_t Af = anchors_of(tbl[fi], B);  // only the first piece's anchors: one dilation per slot
-    if (!Af) continue;
-    const uint32_t bi = f == 0 ? x1 : x0;
-    const uint32_t ci = f == 2 ? x1 : x2;
-    const int p = k < 3 ? __ffsll((unsigned long long)Af) - 1 : 63 - __clzll((long long)Af);
-    const uint64_t B1 = clear_full(B | (tbl[fi].shape << p));
-    uint64_t A2, A3;
-    if (pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3) == 1) return true;
-  }
-  return false;
-}
-
-// quick_slots for one slot k without branches (the rollout kernel): the slot's
-// placement, both leaves and the |D| tests are all computed and combined, so
-// the whole test is one basic block (SIMT runs the leaves anyway whenever any
-// lane of the wave needs them).  Same verdict as quick_slots(B, .., k, 1).
+// In-lane quick test of fixed level-1 slot k of the drawn hand (x0, x1, x2) on
+// B, without branches (the rollout and fused step kernels): the first piece
+// f = k mod 3 at its lowest (k < 3) or highest anchor, then pair_quick's |D|
+// tests and both leaves, all computed and combined, so the whole test is one
+// basic block (SIMT runs the leaves anyway whenever any lane of the wave needs
+// them).  True on an accept (an exact success).
 __device__ __forceinline__ bool quick_slot_bf(uint64_t B, uint32_t x0, uint32_t x1, uint32_t x2, const PieceRow* tbl,
                                               const uint8_t* dtab, int k) {
   const int f = k % 3;
@@ -304,25 +256,6 @@ __device__ __forceinline__ bool quick_hand(uint64_t B, Pcg& rng, uint32_t& ids, 
   return false;
 }
 
-// Exact level-2 search of one slot (both orders), written for ILP: the two
-// orders' G accumulations run side by side and every anchor mask is consumed
-// from both ends (lowest and highest set bit) per iteration, so four
-// independent dependency chains share each loop trip.  Same verdict as
-// one_order(y,z) || one_order(z,y).
-__device__ __forceinline__ uint64_t pop_low(uint64_t& x) {
-  const uint64_t b = x & (~x + 1ull);
-  x ^= b;
-  return b;
-}
-__device__ __forceinline__ uint64_t pop_high(uint64_t& x) {
-  if (!x) return 0ull;
-  const uint64_t b = 1ull << (63 - __clzll((long long)x));
-  x ^= b;
-  return b;
-}
-__device__ __forceinline__ uint64_t and_shifted(uint64_t G, uint64_t bit, uint64_t mlo, uint64_t mhi) {
-  return bit ? G & hi_shl(mlo, mhi, __ffsll((unsigned long long)bit) - 1) : G;
-}
 // Some row or column has at most 5 empty cells (>= 3 filled): a prerequisite
 // for any single placement to complete a line.
 __device__ __forceinline__ bool line_within_reach(uint64_t B) {
@@ -335,119 +268,6 @@ __device__ __forceinline__ bool line_within_reach(uint64_t B) {
     if (__popcll(B & (kCol0 << c)) >= 3) return true;
   return false;
 }
-
-// Exact level-2 search of one slot, phase A (per lane): is there a disjoint
-// placement pair (no line clear needed)?  Written for ILP: the two G
-// accumulations run side by side and every anchor mask is consumed from both
-// ends per trip.  Both G's decide the same question, so the scan stops as
-// soon as EITHER side is exhausted: that side is exact, the other one's
-// partial G only under-reports successes.
-// Returns 1 (yes), 0 (no, and no first placement completes a line), 2 (no
-// disjoint pair: C2 / C3 receive the line-completing anchors of b / c, the
-// only first placements that can still make room for the other piece).
-__device__ __forceinline__ bool completes_line(uint64_t B1, const PieceRow& y, uint64_t bit) {
-  return bit && has_full_line(B1 | (y.shape << (__ffsll((unsigned long long)bit) - 1)));
-}
-
-__device__ __forceinline__ int pair_disjoint(uint64_t B1, const PieceRow& pb, const PieceRow& pc, uint64_t A2,
-                                             uint64_t A3, uint64_t& C2, uint64_t& C3) {
-  // Only the smaller anchor set is scanned (four anchors per trip, two from
-  // each end): G = anchors of the OTHER piece that collide with every
-  // scanned placement; any other-piece anchor outside G gives a disjoint
-  // pair.  G only shrinks, so a hit found early is final.
-  const bool scan3 = __popcll(A3) <= __popcll(A2);
-  const PieceRow& other = scan3 ? pb : pc;  // piece whose anchors G collects
-  const PieceRow& scanned = scan3 ? pc : pb;
-  const uint64_t Aother = scan3 ? A2 : A3;
-  uint64_t mlo, mhi;
-  pair_conflict_mask(other, scanned, mlo, mhi);
-  uint64_t G = ~0ull;
-  uint64_t it = scan3 ? A3 : A2;
-  while (it) {
-    const uint64_t r0 = pop_low(it), r1 = pop_high(it);
-    const uint64_t r2 = pop_low(it), r3 = pop_high(it);
-    G = and_shifted(and_shifted(G, r0, mlo, mhi), r1, mlo, mhi);
-    G = and_shifted(and_shifted(G, r2, mlo, mhi), r3, mlo, mhi);
-    if (Aother & ~G) return 1;
-  }
-  if (!(A2 && A3)) G = ~0ull;  // a piece with no anchor: no disjoint pair
-  if (Aother & ~G) return 1;
-  // no single piece (at most 5 cells across) completes a line with more
-  // than 5 empty cells
-  if (!line_within_reach(B1)) return 0;
-  C2 = 0ull;
-  C3 = 0ull;
-  // four anchors per trip, each piece's set on its own (often one is empty)
-  uint64_t it2 = A2;
-  while (it2) {
-    const uint64_t q0 = pop_low(it2), q1 = pop_high(it2), q2 = pop_low(it2), q3 = pop_high(it2);
-    if (completes_line(B1, pb, q0)) C2 |= q0;
-    if (completes_line(B1, pb, q1)) C2 |= q1;
-    if (completes_line(B1, pb, q2)) C2 |= q2;
-    if (completes_line(B1, pb, q3)) C2 |= q3;
-  }
-  uint64_t it3 = A3;
-  while (it3) {
-    const uint64_t r0 = pop_low(it3), r1 = pop_high(it3), r2 = pop_low(it3), r3 = pop_high(it3);
-    if (completes_line(B1, pc, r0)) C3 |= r0;
-    if (completes_line(B1, pc, r1)) C3 |= r1;
-    if (completes_line(B1, pc, r2)) C3 |= r2;
-    if (completes_line(B1, pc, r3)) C3 |= r3;
-  }
-  return (C2 | C3) ? 2 : 0;
-}
-
-// Phase B (whole wave): every lane's line candidates -- its first-piece
-// anchors C2 (b first) and C3 (c first), all line-completing -- are
-// flattened into one task list and dealt out 64 at a time, so one lane with
-// many candidates no longer holds the wave.  Task: place the first piece,
-// clear, does the second piece fit?  Returns this lane's verdict.  All lanes call it
-// (uniform control flow); lanes without candidates pass C2 = C3 = 0.
-__device__ __forceinline__ bool line_phase_wave(uint64_t B1, uint32_t bi, uint32_t ci, uint64_t C2, uint64_t C3,
-                                                const PieceRow* tbl, int lane) {
-  const uint32_t n2 = (uint32_t)__popcll(C2);
-  const uint32_t cnt = n2 + (uint32_t)__popcll(C3);
-  uint32_t incl = cnt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t u = __shfl_up(incl, o);
-    if (lane >= o) incl += u;
-  }
-  const uint32_t off = incl - cnt;
-  const uint32_t total = (uint32_t)__shfl(incl, 63);
-  uint64_t won = 0ull;  // bit l: lane l's slot succeeded
-#pragma unroll 1
-  for (uint32_t base = 0; base < total; base += 64u) {
-    const uint32_t t = base + (uint32_t)lane;
-    int o = 0;  // owner: last lane with off <= t (and cnt > 0 in range)
-#pragma unroll
-    for (int step = 32; step > 0; step >>= 1) {
-      const int cand = o + step;
-      const uint32_t co = __shfl(off, cand < 64 ? cand : 63);
-      if (cand < 64 && co <= t) o = cand;
-    }
-    const uint64_t oB = __shfl(B1, o);
-    const uint64_t oC2 = __shfl(C2, o), oC3 = __shfl(C3, o);
-    const uint32_t oid = __shfl(bi | (ci << 8), o);
-    const uint32_t k = t - __shfl(off, o);
-    const uint32_t on2 = (uint32_t)__popcll(oC2);
-    bool hit = false;
-    if (t < total) {
-      const bool bfirst = k < on2;
-      const PieceRow& first = tbl[bfirst ? (oid & 0xFFu) : (oid >> 8)];
-      const PieceRow& second = tbl[bfirst ? (oid >> 8) : (oid & 0xFFu)];
-      const int pos = select_bit(bfirst ? oC2 : oC3, bfirst ? k : k - on2);
-      const uint64_t B2 = oB | (first.shape << pos);
-      hit = anchors_of(second, clear_full(B2)) != 0ull;  // candidates complete a line
-    }
-    uint64_t m = hit ? (1ull << o) : 0ull;
-#pragma unroll
-    for (int x = 1; x < 64; x <<= 1) m |= __shfl_xor(m, x);
-    won |= m;
-  }
-  return (won >> lane) & 1ull;
-}
-
 
 // ---------------------------------------------------------------------------
 // Wave64 cross-lane helpers on DPP (gfx9 row_shr / row_bcast): VALU-only, no
@@ -507,17 +327,14 @@ __device__ __forceinline__ uint32_t lds_flag_load_acquire(uint32_t* f) {
 // LDS and taking a prefix max (DPP).  Returns this lane's slot verdict.
 // lds: 64 words of wave-private LDS scratch.  All lanes call it.
 //
-// key (BB_SLOW_EXIT): env << 8 | attempt order of this lane's slot.  A success
+// key (1): env << 8 | attempt order of this lane's slot.  A success
 // decides its env's attempt, so it settles every slot of the same env at the
 // same or a later attempt (those verdicts can no longer change the earliest
 // success); the scan stops once every needed slot is settled or has had all
 // of its tasks.  An attempt that is solvable usually succeeds on its first
 // tasks, so this ends the flattened scan long before its last task.
-#ifndef BB_SLOW_EXIT
-#define BB_SLOW_EXIT 1
-#endif
 //
-// BB_SLOW_LINE_ONLY: one order's leaves suffice where the first placement
+// 1: one order's leaves suffice where the first placement
 // clears nothing.  If c at r completes no line and b then fits, b's anchor is
 // disjoint from c@r on B1, so placing b there first (a clear only frees cells)
 // leaves c@r legal: that b-first leaf succeeds too.  So every leaf of the order
@@ -528,9 +345,6 @@ __device__ __forceinline__ uint32_t lds_flag_load_acquire(uint32_t* f) {
 // sets the launch time -- bb_step's single step (kLineOnly); in the rollout
 // kernel the same code measured -2% (its exact phases are short and the tail
 // averages out over the steps).
-#ifndef BB_SLOW_LINE_ONLY
-#define BB_SLOW_LINE_ONLY 1
-#endif
 #ifndef BB_SLOW_LINE_MIN
 #define BB_SLOW_LINE_MIN 512
 #endif
@@ -538,7 +352,7 @@ template <bool kLineOnly = false>
 __device__ __forceinline__ bool slow_phase_wave(bool need, uint64_t B1, uint32_t bi, uint32_t ci, uint64_t A2,
                                                 uint64_t A3, const PieceRow* tbl, int lane, uint32_t* lds,
                                                 uint32_t key) {
-  if constexpr (kLineOnly && BB_SLOW_LINE_ONLY) {
+  if constexpr (kLineOnly && 1) {
   const uint32_t all = need ? (uint32_t)(__popcll(A2) + __popcll(A3)) : 0u;
   const uint32_t all_tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_add(all), 63);  // every lane
   if (all_tot > (uint32_t)BB_SLOW_LINE_MIN && need) {
@@ -601,15 +415,11 @@ __device__ __forceinline__ bool slow_phase_wave(bool need, uint64_t B1, uint32_t
       hits &= hits - 1;
       const int ol = __builtin_amdgcn_readlane(o, l);
       won_mask |= 1ull << ol;
-#if BB_SLOW_EXIT
       const uint32_t ko = (uint32_t)__builtin_amdgcn_readlane((int)key, ol);
       pending &= ~__ballot((key >> 8) == (ko >> 8) && (key & 0xFFu) >= (ko & 0xFFu));
-#endif
     }
-#if BB_SLOW_EXIT
     pending &= ~__ballot(need && incl <= base + 64u);  // every task of the slot done
     if (!pending) break;
-#endif
   }
   return (won_mask >> lane) & 1ull;
 }
@@ -640,15 +450,6 @@ constexpr int kPack = 32;
 #define BB_MULTI_PASSES 3  // gen_hands_multi: a round packs attempts for up to this many 64-slot passes
 #endif
 constexpr int kMultiPasses = BB_MULTI_PASSES;
-#ifndef BB_PASS_BF
-#define BB_PASS_BF 1  // gen_hands_multi passes: slot decode + pair test without branches (pair_quick_bf)
-#endif
-#ifndef BB_PASS_OWNER_RL
-#define BB_PASS_OWNER_RL 0  // gen_hands_multi passes: slot owner by scalar reads of the attempt offsets (no LDS)
-#endif
-#ifndef BB_PASS_NC
-#define BB_PASS_NC 0  // 1: pass leaf tests without the line clear (pair_quick_nc; measured slower: more exact-phase work)
-#endif
 static_assert(3 * kPack / 2 + 2 <= kJumpMax, "jump table too short for the batch size");
 
 __device__ __forceinline__ void mul128(uint64_t alo, uint64_t ahi, uint64_t blo, uint64_t bhi, uint64_t& lo,
@@ -812,26 +613,12 @@ __device__ __forceinline__ void gen_hand_wave(uint64_t B, Pcg& rng, uint32_t& id
       const uint64_t tq1 = stats ? __builtin_amdgcn_s_memtime() : 0;
       if (stats) stats[4] += (uint32_t)(tq1 - tq0);
       if (needs) {
-#if BB_SLOW_FLAT
         const uint64_t tq2 = stats ? __builtin_amdgcn_s_memtime() : 0;
         ok |= slow_phase_wave(need, B1, bi, ci, A2, A3, tbl, lane, lds, (uint32_t)j);  // one env: attempt j
-        uint64_t C2 = 0ull, C3 = 0ull;
-#else
-        uint64_t C2 = 0ull, C3 = 0ull;
-        if (need) {
-          ok = pair_disjoint(B1, tbl[bi], tbl[ci], A2, A3, C2, C3) == 1;
-        }
-        const uint64_t tq2 = stats ? __builtin_amdgcn_s_memtime() : 0;
-        if (__ballot((C2 | C3) != 0ull)) ok |= line_phase_wave(B1, bi, ci, C2, C3, tbl, lane);
-#endif
         if (stats) {
           const uint64_t tq3 = __builtin_amdgcn_s_memtime();
           stats[5] += (uint32_t)(tq2 - tq1);
           stats[6] += (uint32_t)(tq3 - tq2);
-          uint32_t nt = (uint32_t)(__popcll(C2) + __popcll(C3));
-#pragma unroll
-          for (int x = 1; x < 64; x <<= 1) nt += __shfl_xor(nt, x);
-          stats[7] += nt;
         }
       }
       const uint64_t hit = __ballot(ok);
@@ -975,11 +762,6 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       const int slot = base + lane;
       int j = 0;
       if (nb > 1) {
-#if BB_PASS_OWNER_RL
-        // owner = the number of packed attempt lanes after the first whose first slot is <= this one (their
-        // first slots ascend): one scalar read of each offset, no LDS round trip
-        for (int jj = 1; jj < nb; ++jj) j += slot >= __builtin_amdgcn_readlane(e_off, jj) ? 1 : 0;
-#else
         wave_lds_fence();
         lds[lane] = 0u;
         wave_lds_fence();
@@ -987,7 +769,6 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
           atomicMax(&lds[e_off > base ? e_off - base : 0], (uint32_t)lane);
         wave_lds_fence();
         j = (int)wave_incl_max(lds[lane]);
-#endif
       }
       const uint32_t jid = __shfl(e_ids, j);
       const uint64_t jA0 = __shfl(eA0, j), jA1 = __shfl(eA1, j), jA2 = __shfl(eA2, j);
@@ -996,7 +777,6 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
       int q = 0;
       uint64_t B1 = 0, A2 = 0, A3 = 0;
       uint32_t bi = 0, ci = 0;
-#if BB_PASS_BF
       {  // every lane computes its slot (lanes past `total` a dummy one) and drops it by select
         const int rem0 = slot - joff;
         const int c0 = __popcll(jA0), c1 = __popcll(jA1);
@@ -1010,35 +790,6 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
         q = pair_quick_bf(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
         if (slot >= total) q = 0;
       }
-#else
-      if (slot < total) {
-        int rem = slot - joff;
-        const int c0 = __popcll(jA0), c1 = __popcll(jA1);
-        int f;
-        uint64_t Af;
-        if (rem < c0) {
-          f = 0;
-          Af = jA0;
-        } else if (rem < c0 + c1) {
-          f = 1;
-          Af = jA1;
-          rem -= c0;
-        } else {
-          f = 2;
-          Af = jA2;
-          rem -= c0 + c1;
-        }
-        const int p = select_bit(Af, (uint32_t)rem);
-        bi = hand_id(jid, f == 0 ? 1 : 0);
-        ci = hand_id(jid, f == 2 ? 1 : 2);
-        B1 = clear_full(jB | (tbl[hand_id(jid, f)].shape << p));
-#if BB_PASS_NC
-        q = pair_quick_nc(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
-#else
-        q = pair_quick(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
-#endif
-      }
-#endif
       // attempt lanes with a quick accept: attempt lane L owns the pass's slot
       // bits [lo, hi) of any slot ballot
       const int lo = e_off > base ? e_off - base : 0;

@@ -21,10 +21,13 @@ update.
 Data parallel (one process per GPU, ``torch.distributed.run``): the
 ``num_envs`` envs are split into contiguous shards by global index (seeds
 ``seed + global_index`` as on one GPU); each rank trains on its shard's
-samples with minibatch ``batch_size // world`` so the global minibatch is the
-reference's; gradients are averaged with one RCCL all-reduce of the flat
-gradient buffer per optimizer step and advantage moments are global.
-BatchNorm statistics stay per rank (documented deviation).
+samples with minibatch ``batch_size // world`` (``training.minibatch_scope:
+global``, the default: the global minibatch is the reference's) or
+``batch_size`` (``per_gpu``, SURVEY 8(d) C4: the optimizer steps per update
+are one GPU's); gradients are averaged by an RCCL all-reduce of the flat
+gradient buffer per optimizer step, in buckets issued as backward produces
+them, and advantage moments are global.  BatchNorm statistics stay per rank
+(documented deviation).
 """
 from __future__ import annotations
 
@@ -251,7 +254,17 @@ def train(config: Dict[str, Any], resume_path: Optional[str] = None, seed: int =
     broadcast_parameters(agent)
     if main:
         print(f"Created PPO agent with {sum(p.numel() for p in agent.network.parameters()):,} parameters")
-    local_batch = max(1, agent_cfg.batch_size // world)
+    # minibatch per rank: "global" keeps the reference's global minibatch (batch_size // world per rank, so
+    # the number of optimizer steps per update grows with the world size); "per_gpu" gives every rank a whole
+    # batch_size minibatch of its own shard (per-GPU rollout + per-GPU minibatch 2048; the
+    # effective minibatch is world x batch_size, the optimizer steps per update stay those of one GPU)
+    scope = str(train_cfg.get("minibatch_scope", "global"))
+    if scope not in ("global", "per_gpu"):
+        raise ValueError(f"training.minibatch_scope must be 'global' or 'per_gpu', got {scope!r}")
+    local_batch = agent_cfg.batch_size if scope == "per_gpu" else max(1, agent_cfg.batch_size // world)
+    # data-parallel gradient all-reduce: "graph-split" (two graphs around the bucketed all-reduce) or
+    # "capture" (the collectives captured in the step's graph; nccl = RCCL only)
+    agent.dp_overlap = str(train_cfg.get("dp_overlap", "graph-split"))
     # BASELINE config 5: the rollout step captured in a HIP graph (training.graph_rollout)
     graph_rollout = bool(train_cfg.get("graph_rollout", False)) and device.type == "cuda"
 
@@ -274,7 +287,7 @@ def train(config: Dict[str, Any], resume_path: Optional[str] = None, seed: int =
     if main:
         print(f"\nStarting training for {total_timesteps:,} timesteps...")
         print(f"  Rollout steps: {rollout_steps}")
-        print(f"  Batch size: {agent_cfg.batch_size}")
+        print(f"  Batch size: {agent_cfg.batch_size}" + (f" ({scope}: {local_batch} per rank)" if world > 1 else ""))
         print(f"  Learning rate: {agent_cfg.learning_rate}")
         print("-" * 60, flush=True)
     start = time.time()

@@ -3,7 +3,8 @@
 Needs a build with -DBB_ASYNC_DIAG=1 (python tools/variants.py build adiag, loaded with
 BBVEC_LIB=tools/variants/libbbvec_adiag.so); sets BB_DEBUG_MODE=16.  Reports per env wave:
 iterations per step (T plus blocked iterations), cycles per iteration, blocked env-iterations
-and iterations that moved no env; per search wave: calls, envs per call, cycles per call, polls.
+and iterations that moved no env (and, with -DBB_ASYNC_DIAG=2, the cycles of each phase of an
+iteration); per search wave: calls, envs per call, cycles per call, polls, gen_hands_multi phases.
 """
 import ctypes as C
 import json
@@ -38,16 +39,18 @@ def main():
     buf = np.zeros((n, 4), dtype=np.uint64)
     out = []
     nwe = (n + epw - 1) // epw
-    soff = (n + 31) // 32  # the kernel writes the search waves' counters from here
     nws = (n + epw * ew - 1) // (epw * ew) * sw
+    soff = 16 * nwe  # the kernel writes the search waves' records (16 words each) from here
     for call in range(4):
         env.rollout(T, act[0], rew, term, next_action=act[1], policy_step0=call * T)
         act.reverse()
         torch.cuda.synchronize()
         env.lib.bb_debug_counters(env.handle, buf.ctypes.data_as(C.c_void_p))
         flat = buf.reshape(-1)
-        we = flat[: 4 * nwe].reshape(-1, 4).astype(np.float64)
-        wsx = flat[4 * soff: 4 * soff + 12 * nws].reshape(-1, 12).astype(np.float64)
+        wex = flat[: 16 * nwe].reshape(-1, 16)
+        we = wex[:, :4].astype(np.float64)
+        wsx = flat[soff: soff + 16 * nws].reshape(-1, 16).astype(np.float64)
+        env_ph = wex[:, 4:12].astype(np.float64).sum(axis=0) / we[:, 0].sum()  # cycles per iteration
         ws = wsx[:, :4]
         ph = wsx[:, 4:10].sum(axis=0) / max(ws[:, 0].sum(), 1)  # gen_hands_multi phase cycles per call
         out.append({
@@ -58,8 +61,10 @@ def main():
             "env_wave_cyc_mean": round(we[:, 1].mean(), 0),
             "env_wave_cyc_max": int(we[:, 1].max()),
             "blocked_envs_per_iter_per_wave": round(we[:, 2].sum() / we[:, 0].sum(), 3),
-            "idle_iters_per_wave": round((flat[: 4 * nwe].reshape(-1, 4)[:, 3] & 0xFFFFFFFF).astype(np.float64).mean(), 2),
-            "idle_cyc_frac": round((flat[: 4 * nwe].reshape(-1, 4)[:, 3] >> 32).astype(np.float64).sum() / we[:, 1].sum(), 4),
+            "idle_iters_per_wave": round((wex[:, 3] & 0xFFFFFFFF).astype(np.float64).mean(), 2),
+            "idle_cyc_frac": round((wex[:, 3] >> 32).astype(np.float64).sum() / we[:, 1].sum(), 4),
+            "env_phase_cyc_per_iter": {k: round(float(v), 0) for k, v in zip(
+                ("move_draw", "quick_post", "poll", "philox", "masks", "reward", "outputs_reset", "policy"), env_ph)},
             "search_calls_per_wave": round(ws[:, 0].mean(), 1),
             "envs_per_call": round(ws[:, 1].sum() / max(ws[:, 0].sum(), 1), 2),
             "cyc_per_call": round(ws[:, 2].sum() / max(ws[:, 0].sum(), 1), 0),
