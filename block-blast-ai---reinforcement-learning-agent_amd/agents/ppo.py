@@ -304,7 +304,7 @@ class PPOAgent(BaseAgent):
         # RCCL traffic overlaps the rest of the backward pass; "capture" also captures those collectives
         # inside the optimizer step's HIP graph (one graph per step instead of two around an eager
         # all-reduce; needs the nccl = RCCL backend, opt-in: unmeasured on an 8-GPU node)
-        self.dp_bucket_floats = 1 << 20
+        self.dp_bucket_floats = 1 << 21
         self.dp_overlap = "graph-split"  # or "capture"
         self._dp_hooks = None
         self._dp_hooks_on = True  # off while a graph without collectives is captured

@@ -22,10 +22,16 @@ def main():
         def __init__(self, *a, **k):
             super().__init__(*a, **k)
             captured["agent"] = self
+            captured["steps"] = 0
+
+            def count(_n, _st):
+                captured["steps"] += 1
+            self.minibatch_callback = count
 
     trainer.PPOAgent = Spy
     cfg = {"ppo": {"num_epochs": 1}, "training": {"num_envs": 512, "batch_size": 1024, "rollout_steps": 16,
-                                                  "total_timesteps": 10 ** 9},
+                                                  "total_timesteps": 10 ** 9,
+                                                  "minibatch_scope": os.environ.get("BB_TEST_SCOPE", "global")},
            "logging": {"log_interval": 1, "save_interval": 1000},
            "paths": {"checkpoint_dir": os.path.join(out, "ck"), "log_dir": os.path.join(out, "logs"),
                      "results_dir": os.path.join(out, "res")}}
@@ -35,7 +41,8 @@ def main():
         checksum = float(sum(p.double().sum() for p in agent.network.parameters()))
     rank = dist.get_rank()
     with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
-        json.dump({"checksum": checksum, "total_steps": s["total_steps"], "episodes": s["episodes"]}, f)
+        json.dump({"checksum": checksum, "total_steps": s["total_steps"], "episodes": s["episodes"],
+                   "optimizer_steps": captured["steps"]}, f)
     dist.barrier()
     dist.destroy_process_group()
 

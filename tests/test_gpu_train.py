@@ -83,8 +83,13 @@ def test_episode_window_matches_host_reference_loop(cuda, tmp_path):
     roll.close()
 
 
-def test_data_parallel_two_ranks_stay_in_lockstep(cuda, tmp_path):
-    env = dict(os.environ, BB_DIST_BACKEND="gloo", BB_TEST_OUT=str(tmp_path), MASTER_ADDR="127.0.0.1")
+@pytest.mark.parametrize("scope,steps", [("global", 8), ("per_gpu", 4)])
+def test_data_parallel_two_ranks_stay_in_lockstep(cuda, tmp_path, scope, steps):
+    """Two ranks of 256 envs x 16 steps, batch_size 1,024, one epoch: minibatch_scope "global" gives each
+    rank 512-sample minibatches (8 optimizer steps), "per_gpu" whole 1,024-sample ones (4 steps,
+    SURVEY 8(d) C4); the replicas stay in lockstep either way."""
+    env = dict(os.environ, BB_DIST_BACKEND="gloo", BB_TEST_OUT=str(tmp_path), MASTER_ADDR="127.0.0.1",
+               BB_TEST_SCOPE=scope)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={29600 + os.getpid() % 300}",
            os.path.join(REPO, "tests", "_dist_train_worker.py")]
@@ -94,6 +99,7 @@ def test_data_parallel_two_ranks_stay_in_lockstep(cuda, tmp_path):
     assert res[0]["checksum"] == res[1]["checksum"]  # identical weights after the update
     assert res[0]["total_steps"] == res[1]["total_steps"] == 512 * 16
     assert res[0]["episodes"] == res[1]["episodes"] > 0
+    assert res[0]["optimizer_steps"] == res[1]["optimizer_steps"] == steps
 
 
 def test_data_parallel_graph_step_equals_eager(cuda, tmp_path):
