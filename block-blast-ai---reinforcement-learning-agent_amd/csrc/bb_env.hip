@@ -855,7 +855,9 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
 #define BB_ASYNC_SPRIO 3  // s_setprio of the search waves while they search (0: 5.6e9, 1: 9.58e9, 3: 9.60e9)
 #endif
 #ifndef BB_ASYNC_SLOTS
-#define BB_ASYNC_SLOTS 2  // in-lane quick-test slots per env (1 / 3: 1.078e10 / 1.035e10 vs 1.093e10, r03)
+// in-lane quick-test slots per env: 1 (shipped, r04: 1.277e10) / 2 / 3: 1.246e10 / 1.155e10 (profiles/r04/ab/k1_*);
+// 0: every drawn hand goes to the search waves
+#define BB_ASYNC_SLOTS 1
 #endif
 #ifndef BB_ASYNC_DIAG
 #define BB_ASYNC_DIAG 0  // per-wave counters into dbg_out (tools/diag_async.py, BB_DEBUG_MODE=16); 2: + env-wave
@@ -873,6 +875,9 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
 #endif
 #ifndef BB_ASYNC_SLEEP
 #define BB_ASYNC_SLEEP 1  // s_sleep of an idle search wave between polls
+#endif
+#ifndef BB_ASYNC_LINEONLY
+#define BB_ASYNC_LINEONLY 0  // search waves: slow_phase_wave's line-only second order (BB_SLOW_LINE_MIN tasks up)
 #endif
 #ifndef BB_ASYNC_PHILOX_EARLY
 #define BB_ASYNC_PHILOX_EARLY 0  // the policy uniform computed at the top of every iteration (every lane)
@@ -970,8 +975,8 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
             lds_flag_store_release(&astat[rid], 2u);
           }
         };
-        gen_hands_multi<64>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds, dprof_p, 0,
-                            release);
+        gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
+                                                     a.pack_next, lds, dprof_p, 0, release);
 #if BB_ASYNC_DIAG
         dcyc += __builtin_amdgcn_s_memtime() - c0;
         dcalls += 1;
@@ -1098,9 +1103,9 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     //    success; anything else goes to a search wave, which redraws the attempt)
     if (drew) {
       const uint32_t q0 = s.hand & 63u, q1 = (s.hand >> 6) & 63u, q2 = (s.hand >> 12) & 63u;
-      bool ok = quick_slot_bf(s.B, q0, q1, q2, t.row, t.d, 0);
+      bool ok = false;
 #pragma unroll
-      for (int k = 1; k < BB_ASYNC_SLOTS; ++k) ok = quick_slot_bf(s.B, q0, q1, q2, t.row, t.d, k) || ok;
+      for (int k = 0; k < BB_ASYNC_SLOTS; ++k) ok = quick_slot_bf(s.B, q0, q1, q2, t.row, t.d, k) || ok;
       if (ok) s.rng = after;
       s.hand = (s.hand & 0x3FFFFu) | ((uint32_t)s.rng.has << 22);
       if (ok) {

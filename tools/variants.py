@@ -24,13 +24,19 @@ VARIANTS = {
     # restores them), so their A/B arms cannot be rebuilt from this tree.
     "main": [],
     # bb_rollout (rollout_async_kernel): search waves per workgroup, their priority, in-lane quick-test slots
-    "asw2": ["-DBB_ASYNC_SW=2"],
-    "asw8": ["-DBB_ASYNC_SW=8"],
+    "asw3": ["-DBB_ASYNC_SW=3"],
+    "asw5": ["-DBB_ASYNC_SW=5"],
+    "asw6": ["-DBB_ASYNC_SW=6"],
     "asp2": ["-DBB_ASYNC_SPRIO=2"],
-    "aslot1": ["-DBB_ASYNC_SLOTS=1"],
-    "aslot3": ["-DBB_ASYNC_SLOTS=3"],
+    "aslot0": ["-DBB_ASYNC_SLOTS=0"],
+    "aslot2": ["-DBB_ASYNC_SLOTS=2"],
     "asl4": ["-DBB_ASYNC_SLEEP=4"],
     "aphx": ["-DBB_ASYNC_PHILOX_EARLY=1"],
+    # search waves: the exact phase's line-only second order above BB_SLOW_LINE_MIN tasks
+    "alo0": ["-DBB_ASYNC_LINEONLY=1", "-DBB_SLOW_LINE_MIN=0"],
+    "alo128": ["-DBB_ASYNC_LINEONLY=1", "-DBB_SLOW_LINE_MIN=128"],
+    "alo512": ["-DBB_ASYNC_LINEONLY=1"],
+    "asw8": ["-DBB_ASYNC_SW=8"],
     # per-wave counters of rollout_async_kernel (tools/diag_async.py)
     "adiag": ["-DBB_ASYNC_DIAG=1"],
     "adiag2": ["-DBB_ASYNC_DIAG=2"],
