@@ -77,6 +77,46 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
     }
 
 
+def cpu_baseline_native(seconds: float = 8.0, n: int = 65536, T: int = 16) -> dict:
+    """The same workload on the host's cores through the C-ABI's host backend
+    (libbbvec_host.so, csrc/bb_host.cpp: bitboard step + mask + auto-reset +
+    Philox policy, one env per OpenMP thread iteration) -- the reference's
+    algorithm as native multi-threaded code, beside the port's 1-thread
+    number.  Bounded to ~`seconds`."""
+    import torch
+
+    from runtime.device_env import DeviceEnvBatch
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    e = DeviceEnvBatch(n, seeds=[42 + i for i in range(n)], device="cpu")
+    e.reset()
+    mb = torch.zeros((n, 3), dtype=torch.int64)
+    e.obs(mask_bits=mb)
+    a = [torch.zeros(n, dtype=torch.int32), torch.zeros(n, dtype=torch.int32)]
+    e.random_actions(mb, a[0], seed=POLICY_SEED, step=0)
+    rew = torch.zeros((T, n), dtype=torch.float32)
+    term = torch.zeros((T, n), dtype=torch.uint8)
+    launches = 0
+    t0 = time.perf_counter()
+    while True:
+        e.rollout(T, a[0], rew, term, next_action=a[1], policy_seed=POLICY_SEED, policy_step0=launches * T)
+        a.reverse()
+        launches += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    e.close()
+    return {
+        "value": round(n * T * launches / el, 1),
+        "unit": "env-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n} envs x {T * launches} env-steps ({launches} bb_rollout calls of T={T}, {el:.1f}s), fused "
+                  f"random legal-action policy, host backend libbbvec_host.so (C++ bitboards, OpenMP, "
+                  f"{threads} threads)",
+    }
+
+
 def load_traffic(n_envs: int, mode: str, steps_per_launch: int):
     """HBM bytes per launch from a committed rocprofv3 PMC run
     (profiles/pmc_step_kernel.json or pmc_rollout_kernel.json, written by
@@ -102,6 +142,8 @@ def main() -> None:
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-native-baseline", action="store_true")
+    ap.add_argument("--native-seconds", type=float, default=8.0)
     ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
                     help="rollout: bb_rollout, T fused env-steps per launch (default); step: one bb_step per env-step")
     ap.add_argument("--shards", type=int, default=1,
@@ -254,7 +296,7 @@ def main() -> None:
                 "traffic": traffic,
                 "kernel": (("bb_step = bb::step_kernel + bb::escalate_kernel (BB_STEP_KERNELS=2)"
                             if os.environ.get("BB_STEP_KERNELS") == "2" else
-                            "bb_step = one bb::rollout_kernel<true> launch at T = 1") if args.mode == "step" else
+                            "bb_step = one bb::step_fused_kernel<true> launch") if args.mode == "step" else
                            f"bb_rollout = bb::rollout_async_kernel (env waves + search waves), {T} env-steps "
                            f"of every env per launch"),
                 "env_steps_per_launch": n * per_launch,
@@ -265,6 +307,8 @@ def main() -> None:
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"] = cb
+            if not args.no_native_baseline:
+                out["cpu_baseline_native"] = cpu_baseline_native(args.native_seconds)
         print(json.dumps(out), flush=True)
     for e, _, _, _ in shards:
         e.close()

@@ -634,6 +634,11 @@ constexpr int kStepEnvs = 32;  // envs per wave (two copies per env)
 #define BB_STEP_ROLL_BLOCK 512  // threads per workgroup (8 waves: the SIMD partners in one workgroup)
 #endif
 constexpr int kStepRollBlock = BB_STEP_ROLL_BLOCK;
+#ifndef BB_STEP_QPICK
+#define BB_STEP_QPICK 0  // 0: copy c tests slot c (first piece = hand slot c); 1: the hand's piece of anchor-count
+                         // rank c (quick_rank_bf): 2.90e9 vs 2.94e9 env-steps/s, the extra anchors cost more here
+                         // than the fewer wave searches save (profiles/r04/ab/q2_*)
+#endif
 
 // kStepOut: the bb_step info record and fp64 reward are written when asked for.  The seeded-reset state
 // (seed words, has_seed) is read and expanded only by the envs that terminate, and the PCG64 columns are
@@ -715,7 +720,11 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
   // ---- in-lane quick test of attempt 1, slot `half` of each copy
   const uint32_t idq = lower_half_bcast((uint32_t)ids0 | ((uint32_t)drew0 << 31));
   const uint64_t Bq = ((uint64_t)lower_half_bcast((uint32_t)(s.B >> 32)) << 32) | lower_half_bcast((uint32_t)s.B);
+#if BB_STEP_QPICK
+  if (live && (idq >> 31)) park = !quick_rank_bf(Bq, idq & 63u, (idq >> 6) & 63u, (idq >> 12) & 63u, t.row, t.d, half);
+#else
   if (live && (idq >> 31)) park = !quick_slot_bf(Bq, idq & 63u, (idq >> 6) & 63u, (idq >> 12) & 63u, t.row, t.d, half);
+#endif
   // accept if either copy accepted; else roll back for the wave search
   uint64_t drew_bits = __ballot(live && half == 0 && s.drew);  // copy 1 did not move: copy 0's flags
   drew_bits |= drew_bits << kE;
@@ -858,6 +867,11 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
 // in-lane quick-test slots per env: 1 (shipped, r04: 1.277e10) / 2 / 3: 1.246e10 / 1.155e10 (profiles/r04/ab/k1_*);
 // 0: every drawn hand goes to the search waves
 #define BB_ASYNC_SLOTS 1
+#endif
+#ifndef BB_ASYNC_QPICK
+// 1: the one in-lane slot starts from the hand's fewest-anchor piece (quick_rank_bf), 1.308e10 vs 1.280e10
+// env-steps/s for slot 0 (0; profiles/r04/ab/q1_*)
+#define BB_ASYNC_QPICK 1
 #endif
 #ifndef BB_ASYNC_DIAG
 #define BB_ASYNC_DIAG 0  // per-wave counters into dbg_out (tools/diag_async.py, BB_DEBUG_MODE=16); 2: + env-wave
@@ -1104,8 +1118,12 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
     if (drew) {
       const uint32_t q0 = s.hand & 63u, q1 = (s.hand >> 6) & 63u, q2 = (s.hand >> 12) & 63u;
       bool ok = false;
+#if BB_ASYNC_QPICK
+      ok = quick_rank_bf(s.B, q0, q1, q2, t.row, t.d, 0);
+#else
 #pragma unroll
       for (int k = 0; k < BB_ASYNC_SLOTS; ++k) ok = quick_slot_bf(s.B, q0, q1, q2, t.row, t.d, k) || ok;
+#endif
       if (ok) s.rng = after;
       s.hand = (s.hand & 0x3FFFFu) | ((uint32_t)s.rng.has << 22);
       if (ok) {

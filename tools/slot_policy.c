@@ -113,7 +113,7 @@ static void order_by_anchors(uint64_t B, const int h[3], int ord[3], int* nz) {
   for (int i = 0; i < 3; ++i) { ord[i] = o2[i]; if (cnt[o2[i]]) (*nz)++; }
 }
 
-enum { NPOL = 17 };
+enum { NPOL = 24 };
 static const char* pol_names[NPOL] = {
   "shipped: f0 low | f1 low",
   "f0 low | f0 high",
@@ -132,6 +132,13 @@ static const char* pol_names[NPOL] = {
   "shipped slots, leaves without clears",
   "most cells low | 2nd most cells low",
   "most cells low | most cells high",
+  "1 slot: f0 low",
+  "1 slot: f0 high",
+  "1 slot: least-anchors low",
+  "1 slot: most cells low",
+  "1 slot: most-anchors low",
+  "1 slot: f0 low, +last leaf",
+  "1 slot: most cells low, +last leaf",
 };
 static uint64_t acc_cnt[NPOL], n_first, n_ok;
 enum { KMAX = 16 };
@@ -184,6 +191,13 @@ static void gen_hook(const struct Engine* ee, int attempt, int ok) {
         if (g_pieces[h[oc[j]]].n > g_pieces[h[oc[i]]].n) { int t = oc[i]; oc[i] = oc[j]; oc[j] = t; }
     r[15] = slot_test(B, h, oc[0], 0, 0) | slot_test(B, h, oc[1], 0, 0);
     r[16] = slot_test(B, h, oc[0], 0, 0) | slot_test(B, h, oc[0], 1, 0);
+    r[17] = slot_test(B, h, 0, 0, 0);
+    r[18] = slot_test(B, h, 0, 1, 0);
+    r[19] = slot_test(B, h, ord[0], 0, 0);
+    r[20] = slot_test(B, h, oc[0], 0, 0);
+    r[21] = slot_test(B, h, nz ? ord[nz - 1] : 0, 0, 0);
+    r[22] = slot_test(B, h, 0, 0, 1);
+    r[23] = slot_test(B, h, oc[0], 0, 1);
   }
   {
     /* fixed list: round j covers (f0,f1,f2) at the j/2-th anchor from the low (even j) or high (odd j) end */

@@ -31,6 +31,10 @@ VARIANTS = {
     "aslot0": ["-DBB_ASYNC_SLOTS=0"],
     "aslot2": ["-DBB_ASYNC_SLOTS=2"],
     "asl4": ["-DBB_ASYNC_SLEEP=4"],
+    # the one in-lane slot starts from the fewest-anchor piece (quick_least_bf)
+    "aqp0": ["-DBB_ASYNC_QPICK=0"],
+    # bb_step (step_fused_kernel): copy c's slot from the anchor-count rank c instead of hand slot c
+    "sqp1": ["-DBB_STEP_QPICK=1"],
     "aphx": ["-DBB_ASYNC_PHILOX_EARLY=1"],
     # search waves: the exact phase's line-only second order above BB_SLOW_LINE_MIN tasks
     "alo0": ["-DBB_ASYNC_LINEONLY=1", "-DBB_SLOW_LINE_MIN=0"],
