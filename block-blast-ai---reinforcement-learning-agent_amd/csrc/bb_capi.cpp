@@ -873,43 +873,3 @@ extern "C" int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const
   return BB_OK;
 }
 
-extern "C" int64_t bb_relu_bias_grad_workspace_bytes(int32_t rows, int32_t cols) {
-  return relu_bgrad_workspace_bytes(rows, cols);
-}
-
-extern "C" int bb_relu_bias_grad(const void* d_gy, const void* d_y, int32_t dtype, int32_t rows, int32_t cols,
-                                 float* d_ws, void* d_g, void* d_db, void* stream) {
-  if (dtype != 1) return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: bf16 (dtype 1) only");
-  if (rows <= 0 || cols <= 0 || cols % 64 != 0)
-    return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: rows > 0 and a multiple of 64 columns");
-  if (!d_gy || !d_y || !d_g || !d_db || !d_ws) return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: NULL argument");
-  if (!al16(d_gy) || !al16(d_y) || !al16(d_g))
-    return fail(nullptr, BB_ERR_ARG, "bb_relu_bias_grad: tensors must be 16-byte aligned");
-  hipError_t st = launch_relu_bgrad(d_gy, d_y, rows, cols, d_g, d_db, d_ws, (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_relu_bias_grad");
-  return BB_OK;
-}
-
-extern "C" int64_t bb_conv_in_workspace_bytes(int32_t N) { return conv_in_wgrad_workspace_bytes(N); }
-
-extern "C" int bb_conv_in_forward(const float* d_x, const float* d_w, int32_t w_layout, int32_t N, void* d_y,
-                                  void* stream) {
-  if (N <= 0 || (w_layout != 0 && w_layout != 1))
-    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: N > 0, w_layout 0 or 1");
-  if (!d_x || !d_w || !d_y) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: NULL argument");
-  if (!al16(d_x) || !al16(d_y)) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: x, y must be 16-byte aligned");
-  hipError_t st = launch_conv_in_forward(d_x, d_w, w_layout, N, d_y, (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_forward");
-  return BB_OK;
-}
-
-extern "C" int bb_conv_in_wgrad(const float* d_x, const void* d_dy, int32_t N, float* d_ws, int32_t w_layout,
-                                float* d_dw, void* stream) {
-  if (N <= 0 || (w_layout != 0 && w_layout != 1))
-    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: N > 0, w_layout 0 or 1");
-  if (!d_x || !d_dy || !d_ws || !d_dw) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: NULL argument");
-  if (!al16(d_x) || !al16(d_dy)) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: x, dy must be 16-byte aligned");
-  hipError_t st = launch_conv_in_wgrad(d_x, d_dy, N, d_ws, w_layout, d_dw, (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_wgrad");
-  return BB_OK;
-}

@@ -490,6 +490,175 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
 }
 
 // ---------------------------------------------------------------------------
+// forward / data gradient, weight-stationary (the shipped path without the
+// statistics epilogue).  conv_fwd_kernel streams the whole weight tensor from
+// L2 through LDS for every 2 boards (295 KB per 37.7 MFLOP at 128 -> 128:
+// ~300 MB of L2 reads per 2,048-board call, and a barrier per tap stage).
+// Here each workgroup is persistent (one per CU, one wave per SIMD) and holds
+// its weights in registers for all of its boards: wave w owns output channels
+// [w CW, (w + 1) CW), CW = COUT / 4, as mfma_f32_16x16x32_bf16 A fragments
+// (CW / 16 tiles x 9 CIN / 32 k-steps x 4 VGPRs: 288 at 128 -> 128), loaded
+// once.  The boards stream through a ring of kWsBuf LDS slots (64 pixel rows +
+// 16 zero rows each, the swizzle of conv_fwd_kernel) by direct global -> LDS
+// copies issued two boards ahead; per board a wave reads its B fragments (4
+// pixel tiles per k-step, ds_read_b128, the next k-step's issued before this
+// one's MFMAs) and runs CW / 16 x 4 x KS MFMAs, then stores 4 channels x 1
+// pixel per lane and tile (8 bytes).  One barrier per board.  The LDS address
+// of a B fragment is base[t][i] ^ (cb << 6): base holds the tap's shifted row
+// (or its zero row), the lane's chunk and the slot, and the 32-channel block cb
+// only flips chunk bits (row offsets are multiples of 128 bytes, slot offsets
+// of 2 KiB).
+// ---------------------------------------------------------------------------
+constexpr int kWsBuf = 3;
+#ifndef BB_CONV_WS_WAIT
+#define BB_CONV_WS_WAIT 0
+#endif
+constexpr int kWsZero = 16;
+
+int ws_grid(int nb) {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cus[dev]) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus[dev] = c;
+  }
+  return nb < cus[dev] ? nb : cus[dev];
+}
+
+template <int CIN, int COUT>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int nb,
+                   const uint16_t* __restrict__ radd) {
+  constexpr int RB = CIN * 2;                       // bytes per pixel row
+  constexpr int NCH = CIN / 8;                      // 16-byte chunks per pixel row
+  constexpr int SLOT = (64 + kWsZero) * RB;         // one board + its zero rows
+  constexpr int NCB = CIN / 32;                     // 32-channel blocks per tap
+  constexpr int KS = 9 * NCB;                       // k-steps
+  constexpr int CW = COUT / 4;                      // output channels per wave
+  constexpr int NT = CW / 16;                       // 16-channel tiles per wave
+  constexpr int LPW = 64 * NCH / 256;               // direct copies per lane per board
+  static_assert(NT >= 1 && LPW >= 1, "shape");
+  __shared__ __attribute__((aligned(16))) uint8_t sm[kWsBuf * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, hq = lane >> 4;
+  const int G = gridDim.x;
+  const int co0 = wid * CW;
+
+  // copies of board b into slot s: LDS chunk e = 256 k + tid holds row e / NCH, logical chunk (e % NCH) ^ key
+  auto copy_board = [&](int b, int s) {
+    const uint16_t* src = x + (size_t)min(b, nb - 1) * 64 * CIN;
+#pragma unroll
+    for (int k = 0; k < LPW; ++k) {
+      const int e = k * 256 + tid, r = e / NCH, lc = (e % NCH) ^ fwd_key<CIN>(r);
+      glds16_async(src + r * CIN + lc * 8, sm + s * SLOT + (k * 256 + wid * 64) * 16);
+    }
+  };
+  const int b0 = blockIdx.x;
+  copy_board(b0, 0);
+  // weights -> registers: A fragment of tile j, k-step s: co = co0 + 16 j + r16, ci = 32 cb + 8 hq .. + 7 of tap t
+  // (issued in k-step order, so the first board's MFMAs start as the first fragments arrive)
+  bf16x8 wa[NT][KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      wa[j][s] = *reinterpret_cast<const bf16x8*>(w + ((size_t)(s / NCB) * COUT + co0 + 16 * j + r16) * CIN +
+                                                  32 * (s % NCB) + 8 * hq);
+  copy_board(b0 + G, 1);
+  // zero rows of every slot (never overwritten: the copies fill rows 0..63 only)
+  for (int i = tid; i < kWsBuf * kWsZero * NCH; i += 256) {
+    const int s = i / (kWsZero * NCH), j = i % (kWsZero * NCH);
+    *reinterpret_cast<uint4*>(sm + s * SLOT + 64 * RB + j * 16) = make_uint4(0, 0, 0, 0);
+  }
+  // base[t][i]: byte address in slot 0 of chunk (hq ^ key) of the row that pixel 16 i + r16 reads at tap t
+  int base[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const int p = 16 * i + r16, yy = (p >> 3) + dy, xc = (p & 7) + dx;
+      const int row = ((unsigned)yy < 8u && (unsigned)xc < 8u) ? yy * 8 + xc : 64 + ((p + 8 * dy + dx) & 15);
+      base[t][i] = row * RB + ((hq ^ fwd_key<CIN>(row)) << 4);
+    }
+  // board 0's copies have landed (the weight fragments and board 1's copies are younger and may be in flight:
+  // the compiler waits for each fragment before its first use)
+#if BB_CONV_WS_WAIT
+  BB_WAIT_VM_LGKM0(0);  // variant: every weight fragment (and board 1) has landed before the loop
+#else
+  BB_WAIT_VM_LGKM0(NT * KS + LPW);
+#endif
+  raw_barrier();
+
+  int slot = 0;
+  for (int b = b0; b < nb; b += G) {
+    // board b + 2 G into the slot board b - G used (every wave passed the barrier after reading it)
+    const int s2 = slot == 0 ? 2 : slot - 1;
+    copy_board(b + 2 * G, s2);
+    uint2 ra[NT][4];
+    if (radd) {  // block-uniform
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          ra[j][i] = *reinterpret_cast<const uint2*>(radd + ((size_t)b * 64 + 16 * i + r16) * COUT + co0 + 16 * j +
+                                                     4 * hq);
+    }
+    f32x4 acc[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 bfr[2][4];
+    auto load = [&](int s, int set) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        bfr[set][i] = *reinterpret_cast<const bf16x8*>(sm + (base[s / NCB][i] ^ ((s % NCB) << 6)));
+    };
+    load(0, 0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s + 1 < KS) load(s + 1, (s + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][s], bfr[s & 1][i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // lane holds D[co0 + 16 j + 4 hq + reg][16 i + r16]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        uint2 v;
+        v.x = pack2(acc[j][i][0], acc[j][i][1]);
+        v.y = pack2(acc[j][i][2], acc[j][i][3]);
+        if (radd) v = make_uint2(add2_bf16(v.x, ra[j][i].x), add2_bf16(v.y, ra[j][i].y));
+        *reinterpret_cast<uint2*>(y + ((size_t)b * 64 + 16 * i + r16) * COUT + co0 + 16 * j + 4 * hq) = v;
+      }
+    // next slot: its board's copies (issued one board earlier) must have landed for every wave.  Younger than
+    // them: this board's stores (NT * 4) and the copies of board b + 2 G (LPW) -- and, before those, the
+    // previous board's stores; waiting for at most LPW + 4 NT outstanding is therefore enough (and the radd
+    // loads, when present, already drained everything older)
+    BB_WAIT_VM(LPW + 4 * NT);
+    raw_barrier();
+    const int delta = slot == kWsBuf - 1 ? -(kWsBuf - 1) * SLOT : SLOT;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) base[t][i] += delta;
+    slot = slot == kWsBuf - 1 ? 0 : slot + 1;
+  }
+  BB_WAIT_VM(0);  // no copy into this workgroup's LDS may outlive it
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient.  Workgroup (8 waves): one 64 (co) x 64 (ci) tile, all nine
 // taps, over a chunk of boards, 2 boards per LDS stage.  Stages go through a
 // ring of 4 LDS buffers by direct global -> LDS copies issued 3 stages ahead;
@@ -751,9 +920,20 @@ int wgrad_bpc(int nb, int nchunk) {
   return (bpc + kWgBoards - 1) / kWgBoards * kWgBoards;
 }
 
+#ifndef BB_CONV_FWD_WS
+#define BB_CONV_FWD_WS 0  // 1: forward / data gradient on conv_fwd_ws_kernel (parity-green, first build 46.2 vs
+                          // 42.2 us per 128 -> 128 call: in work); the statistics epilogue always uses conv_fwd_kernel
+#endif
+
 template <int CIN, int COUT>
 hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr,
                  const float* pb = nullptr, double* part = nullptr) {
+  if (nb <= 0) return hipErrorInvalidValue;
+  if (BB_CONV_FWD_WS && !part) {
+    hipLaunchKernelGGL((conv_fwd_ws_kernel<CIN, COUT>), dim3(ws_grid(nb)), dim3(256), 0, s, (const uint16_t*)x,
+                       (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd);
+    return hipGetLastError();
+  }
   if ((radd || part) && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS))
     return hipErrorInvalidValue;  // variant builds: no fused add / statistics
   hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>()), dim3(kFwdThreads), 0, s,
@@ -775,131 +955,6 @@ hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, flo
   hipLaunchKernelGGL(conv_wgrad_reduce, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ws, used, COUT,
                      CIN, wl, dw);
   return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// The input layer (the first Conv2d 4 -> 64 of the conv stack, network.py:75-117)
-// under bf16 autocast: x f32 NHWC [N][8][8][4] and the f32 weight are rounded to
-// bf16 in-kernel (autocast's casts), f32 accumulation, y bf16 NHWC
-// [N][64 px][64] without bias.  0.6 GFLOP per 2,048 boards: no MFMA tiling, one
-// thread per pixel and all 64 output channels (weights broadcast from LDS).
-// Weight gradient: thread (co, ci) of a workgroup accumulates the nine taps over
-// kInWgBoards boards -> partials [chunk][t][co][ci], summed in chunk order by
-// conv_wgrad_reduce (no atomics, deterministic).  MIOpen's version of this layer
-// cost a split-K weight-gradient kernel plus zero fills and casts.
-// ---------------------------------------------------------------------------
-constexpr int kInCout = 64, kInCin = 4;
-constexpr int kInCg = 16;        // forward: output channels per thread (4 channel groups x 64 pixels = 256 threads)
-constexpr int kInWgBoards = 8;   // weight gradient: boards per workgroup
-constexpr int kInWgThreads = 512;
-
-__device__ __forceinline__ float bf16r(float f) { return __uint_as_float(uint32_t(f2bf(f)) << 16); }
-
-// forward: kInBoards boards per workgroup (the weight staging amortised over them); wave g computes channels
-// [16g, 16g + 16) of a board's 64 pixels (weights broadcast from LDS)
-constexpr int kInBoards = 1;  // 1: 28.8 us per 2,048 boards; 4 (staging amortised, boards looped): slower
-__global__ void __launch_bounds__(kThreads) conv_in_fwd_kernel(const float* __restrict__ x,
-                                                               const float* __restrict__ w, int wl, int nb,
-                                                               uint16_t* __restrict__ y) {
-  __shared__ float4 ws[kInCout][9];           // [co][t] = 4 input channels, rounded to bf16
-  __shared__ float4 xs[kInBoards * 64 + 1];   // + one zero row for off-board taps
-  for (int i = threadIdx.x; i < kInCout * 9; i += kThreads) {
-    const int co = i / 9, t = i % 9;
-    float v[kInCin];
-#pragma unroll
-    for (int ci = 0; ci < kInCin; ++ci) v[ci] = bf16r(w[wl ? (co * 9 + t) * kInCin + ci : (co * kInCin + ci) * 9 + t]);
-    ws[co][t] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-  const int b0 = blockIdx.x * kInBoards, nbb = min(kInBoards, nb - b0);
-  for (int i = threadIdx.x; i < kInBoards * 64; i += kThreads) {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < nbb * 64) {
-      v = reinterpret_cast<const float4*>(x)[(size_t)b0 * 64 + i];
-      v = make_float4(bf16r(v.x), bf16r(v.y), bf16r(v.z), bf16r(v.w));
-    }
-    xs[i] = v;
-  }
-  if (threadIdx.x == 0) xs[kInBoards * 64] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-  const int p = threadIdx.x & 63, cg = threadIdx.x >> 6;
-  const int py = p >> 3, pc = p & 7;
-  for (int bb = 0; bb < nbb; ++bb) {
-    float4 patch[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int yy = py + t / 3 - 1, xc = pc + t % 3 - 1;
-      patch[t] = xs[((unsigned)yy < 8u && (unsigned)xc < 8u) ? bb * 64 + yy * 8 + xc : kInBoards * 64];
-    }
-    float acc[kInCg];
-#pragma unroll
-    for (int j = 0; j < kInCg; ++j) {
-      float a = 0.f;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const float4 q = ws[cg * kInCg + j][t];
-        a += q.x * patch[t].x;
-        a += q.y * patch[t].y;
-        a += q.z * patch[t].z;
-        a += q.w * patch[t].w;
-      }
-      acc[j] = a;
-    }
-    uint4* yo = reinterpret_cast<uint4*>(y + ((size_t)(b0 + bb) * 64 + p) * kInCout + cg * kInCg);
-    yo[0] = make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
-    yo[1] = make_uint4(pack2(acc[8], acc[9]), pack2(acc[10], acc[11]), pack2(acc[12], acc[13]),
-                       pack2(acc[14], acc[15]));
-  }
-}
-
-// weight gradient: thread (co, pixel group) accumulates all 36 (ci, t) products of its pixels; the
-// 8 pixel groups add through LDS in a fixed order -> partials [chunk][t][co][ci]
-__global__ void __launch_bounds__(kInWgThreads) conv_in_wgrad_kernel(const float* __restrict__ x,
-                                                                     const uint16_t* __restrict__ dy, int nb,
-                                                                     float* __restrict__ part) {
-  constexpr int PG = kInWgThreads / kInCout;  // pixel groups
-  __shared__ float4 xs[kInWgBoards * 64 + 1];
-  __shared__ float red[PG][36][kInCout + 1];
-  const int co = threadIdx.x & (kInCout - 1), pg = threadIdx.x >> 6;
-  const int b0 = blockIdx.x * kInWgBoards;
-  const int nbb = min(kInWgBoards, nb - b0);
-  for (int i = threadIdx.x; i < kInWgBoards * 64; i += kInWgThreads) {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < nbb * 64) {
-      v = reinterpret_cast<const float4*>(x)[(size_t)b0 * 64 + i];
-      v = make_float4(bf16r(v.x), bf16r(v.y), bf16r(v.z), bf16r(v.w));
-    }
-    xs[i] = v;
-  }
-  if (threadIdx.x == 0) xs[kInWgBoards * 64] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-  float acc[36];
-#pragma unroll
-  for (int k = 0; k < 36; ++k) acc[k] = 0.f;
-  for (int p = pg; p < nbb * 64; p += PG) {  // dy read straight from global (coalesced 128 B per wave)
-    const float g = __uint_as_float(uint32_t(dy[((size_t)b0 * 64 + p) * kInCout + co]) << 16);
-    const int q = p & 63, py = q >> 3, pc = q & 7;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int yy = py + t / 3 - 1, xc = pc + t % 3 - 1;
-      const float4 v = xs[((unsigned)yy < 8u && (unsigned)xc < 8u) ? (p & ~63) + yy * 8 + xc : kInWgBoards * 64];
-      acc[0 * 9 + t] += g * v.x;
-      acc[1 * 9 + t] += g * v.y;
-      acc[2 * 9 + t] += g * v.z;
-      acc[3 * 9 + t] += g * v.w;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 36; ++k) red[pg][k][co] = acc[k];
-  __syncthreads();
-  const size_t n = (size_t)9 * kInCout * kInCin;
-  for (int i = threadIdx.x; i < 36 * kInCout; i += kInWgThreads) {
-    const int k = i / kInCout, c = i % kInCout;  // k = ci * 9 + t
-    float s = 0.f;
-#pragma unroll
-    for (int g2 = 0; g2 < PG; ++g2) s += red[g2][k][c];
-    const int ci = k / 9, t = k % 9;
-    part[blockIdx.x * n + (t * kInCout + c) * kInCin + ci] = s;
-  }
 }
 
 }  // namespace
@@ -940,29 +995,6 @@ hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int
   }
   tab.block0[count] = blocks;
   hipLaunchKernelGGL(conv_prep_multi_kernel, dim3(blocks), dim3(kThreads), 0, s, tab);
-  return hipGetLastError();
-}
-
-int64_t conv_in_wgrad_workspace_bytes(int nb) {
-  if (nb <= 0) return -1;
-  return (int64_t)((nb + kInWgBoards - 1) / kInWgBoards) * 9 * kInCout * kInCin * (int64_t)sizeof(float);
-}
-
-hipError_t launch_conv_in_forward(const float* x, const float* w, int wl, int nb, void* y, hipStream_t s) {
-  if (nb <= 0 || (wl != 0 && wl != 1)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_in_fwd_kernel, dim3((nb + kInBoards - 1) / kInBoards), dim3(kThreads), 0, s, x, w, wl, nb,
-                     static_cast<uint16_t*>(y));
-  return hipGetLastError();
-}
-
-hipError_t launch_conv_in_wgrad(const float* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s) {
-  if (nb <= 0 || (wl != 0 && wl != 1)) return hipErrorInvalidValue;
-  const int nchunk = (nb + kInWgBoards - 1) / kInWgBoards;
-  hipLaunchKernelGGL(conv_in_wgrad_kernel, dim3(nchunk), dim3(kInWgThreads), 0, s, x,
-                     static_cast<const uint16_t*>(dy), nb, ws);
-  const int n = 9 * kInCout * kInCin;
-  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ws, nchunk,
-                     kInCout, kInCin, wl, dw);
   return hipGetLastError();
 }
 

@@ -116,9 +116,6 @@ int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout);
 hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* wf, void* wd, hipStream_t s);
 hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
                                      const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s);
-int64_t conv_in_wgrad_workspace_bytes(int nb);
-hipError_t launch_conv_in_forward(const float* x, const float* w, int wl, int nb, void* y, hipStream_t s);
-hipError_t launch_conv_in_wgrad(const float* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s);
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
                                   const void* radd = nullptr, const float* pb = nullptr, double* part = nullptr);
 int conv3x3_stats_parts(int nb, int cout);
@@ -143,9 +140,6 @@ int64_t adam_clip_workspace_bytes(int count, const int64_t* n);
 hipError_t launch_adam_clip(int count, float* const* p, float* const* g, float* const* m, float* const* v,
                             float* const* step, const int64_t* n, double lr, double beta1, double beta2, double eps,
                             float max_norm, double* ws, float* norm_out, hipStream_t s);
-int64_t relu_bgrad_workspace_bytes(int rows, int cols);
-hipError_t launch_relu_bgrad(const void* gy, const void* y, int rows, int cols, void* g, void* db, float* ws,
-                             hipStream_t s);
 hipError_t launch_cast_multi(int count, int dir, const void* const* src, void* const* dst, const int64_t* n,
                              const int32_t* perm_c, const int32_t* perm_hw, hipStream_t s);
 

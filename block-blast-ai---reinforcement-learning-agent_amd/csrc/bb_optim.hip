@@ -260,57 +260,6 @@ __global__ void __launch_bounds__(kOptThreads) cast_multi_kernel(const CastTable
   }
 }
 
-// ReLU backward + bias gradient of a bf16 Linear -> ReLU (LinearReLUFunction):
-// g = (y <= 0) ? 0 : gy (threshold_backward), db[c] = sum over rows of g (f32,
-// fixed order, rounded to bf16 as torch's bf16 sum).  Pass 1: one workgroup per
-// 64 rows x 64 columns (8 columns per thread, 16-byte loads) writes g and f32
-// column partials; pass 2 adds the row-chunk partials in order.  (One workgroup
-// per 64 columns over all rows was latency-bound: slower than torch's pair.)
-constexpr int kRbThreads = 512;
-constexpr int kRbRows = 64;
-__global__ void __launch_bounds__(kRbThreads) relu_bgrad_kernel(const uint16_t* __restrict__ gy,
-                                                               const uint16_t* __restrict__ y, int rows, int cols,
-                                                               uint16_t* __restrict__ g, float* __restrict__ part) {
-  __shared__ float red[kRbThreads / 8][64 + 1];
-  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;  // 8 column octets x 64 rows
-  const int c0 = blockIdx.x * 64 + cg * 8;
-  const int r = blockIdx.y * kRbRows + rg;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (r < rows) {
-    const int64_t o = (int64_t)r * cols + c0;
-    const uint4 a = *reinterpret_cast<const uint4*>(gy + o);
-    const uint4 b = *reinterpret_cast<const uint4*>(y + o);
-    const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-    uint32_t ov[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t lo_keep = bf2f(uint16_t(bv[k])) <= 0.f ? 0u : 0xFFFFu;
-      const uint32_t hi_keep = bf2f(uint16_t(bv[k] >> 16)) <= 0.f ? 0u : 0xFFFF0000u;
-      ov[k] = av[k] & (lo_keep | hi_keep);
-      acc[2 * k] = bf2f(uint16_t(ov[k]));
-      acc[2 * k + 1] = bf2f(uint16_t(ov[k] >> 16));
-    }
-    *reinterpret_cast<uint4*>(g + o) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[rg][cg * 8 + j] = acc[j];
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    float s = 0.f;
-    for (int i = 0; i < kRbRows; ++i) s += red[i][threadIdx.x];
-    part[(int64_t)blockIdx.y * cols + blockIdx.x * 64 + threadIdx.x] = s;
-  }
-}
-
-__global__ void __launch_bounds__(256) relu_bgrad_sum_kernel(const float* __restrict__ part, int chunks, int cols,
-                                                             uint16_t* __restrict__ db) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int i = 0; i < chunks; ++i) s += part[(int64_t)i * cols + c];
-  db[c] = f2bf_rne(s);
-}
-
 int build_adam_table(AdamTable& tab, int count, float* const* p, float* const* g, float* const* m, float* const* v,
                      float* const* step, const int64_t* n) {
   if (count <= 0 || count > kOptMaxTensors) return -1;
@@ -354,23 +303,6 @@ hipError_t launch_adam_clip(int count, float* const* p, float* const* g, float* 
   hipLaunchKernelGGL(adam_finalize_kernel, dim3(1), dim3(kOptThreads), 0, s, tab, ws, max_norm, beta1, beta2,
                      norm_out);
   hipLaunchKernelGGL(adam_update_kernel, dim3(chunks), dim3(kOptThreads), 0, s, tab, ws, lr, beta1, beta2, eps);
-  return hipGetLastError();
-}
-
-int64_t relu_bgrad_workspace_bytes(int rows, int cols) {
-  if (rows <= 0 || cols <= 0) return -1;
-  return int64_t((rows + kRbRows - 1) / kRbRows) * cols * int64_t(sizeof(float));
-}
-
-hipError_t launch_relu_bgrad(const void* gy, const void* y, int rows, int cols, void* g, void* db, float* ws,
-                             hipStream_t s) {
-  if (rows <= 0 || cols <= 0 || cols % 64 != 0) return hipErrorInvalidValue;
-  const int chunks = (rows + kRbRows - 1) / kRbRows;
-  hipLaunchKernelGGL(relu_bgrad_kernel, dim3(cols / 64, chunks), dim3(kRbThreads), 0, s,
-                     static_cast<const uint16_t*>(gy), static_cast<const uint16_t*>(y), rows, cols,
-                     static_cast<uint16_t*>(g), ws);
-  hipLaunchKernelGGL(relu_bgrad_sum_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, ws, chunks, cols,
-                     static_cast<uint16_t*>(db));
   return hipGetLastError();
 }
 

@@ -58,9 +58,6 @@ class BatchNorm2d(nn.BatchNorm2d):
 
 
 HIP_CONV = os.environ.get("BB_HIP_CONV", "1") != "0"  # 3x3 64/128-channel convs on csrc/bb_conv.hip under bf16
-# the 4 -> 64 input layer on csrc/bb_conv.hip too: bit-deterministic bf16 step, but measured +0.6% on the update
-# step against MIOpen's (its forward is LDS-latency-bound, 28.8 us vs 11.5 + a 5 us cast): opt-in
-HIP_CONV_IN = os.environ.get("BB_HIP_CONV_IN", "0") == "1"
 NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last trunk: flatten without the layout copy
 FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"  # bf16 Linear weights/biases cast in one launch each way
 CAST_PERM_ROW_MAX = 8192  # bb_cast_multi's permuted-row limit (perm_c * perm_hw, include/bbvec.h)
@@ -86,12 +83,10 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> 
     autocast's conv2d.  ``images``: {conv: bf16 weight images} prepared for all
     layers in one launch (BlockBlastNetwork._conv_images)."""
     if _hip_conv_on(x):
-        from runtime.kernels import Conv3x3Function, ConvInFunction, conv3x3_fusable, conv_in_fusable
+        from runtime.kernels import Conv3x3Function, conv3x3_fusable
 
         if conv3x3_fusable(x, conv):
             return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox)
-        if HIP_CONV_IN and conv_in_fusable(x, conv):  # the 4 -> 64 input layer
-            return ConvInFunction.apply(x, conv.weight)
     return conv._conv_forward(x, conv.weight, None)
 
 

@@ -381,50 +381,6 @@ class GradMailbox:
         return g
 
 
-def conv_in_fusable(x: torch.Tensor, conv) -> bool:
-    """The conv stack's input layer (4 -> 64, 3x3 / stride 1 / pad 1) applied to
-    f32 8x8 boards that need no input gradient (the network input)."""
-    return (x.is_cuda and x.dim() == 4 and tuple(x.shape[1:]) == (4, 8, 8) and x.shape[0] > 0
-            and x.dtype == torch.float32 and not x.requires_grad and conv.in_channels == 4
-            and conv.out_channels == 64 and conv.groups == 1 and tuple(conv.kernel_size) == (3, 3)
-            and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1) and tuple(conv.dilation) == (1, 1)
-            and conv.padding_mode == "zeros")
-
-
-class ConvInFunction(torch.autograd.Function):
-    """The input layer conv2d(x, weight, padding=1) without bias under bf16
-    autocast (bb_conv_in_forward / bb_conv_in_wgrad): x and weight rounded to
-    bf16 as autocast's casts, f32 accumulation, bf16 NHWC output, f32 weight
-    gradient; no input gradient (the network input has none)."""
-
-    @staticmethod
-    def forward(ctx, x, weight):
-        _need_cuda(x, weight)
-        x = x.contiguous(memory_format=torch.channels_last)
-        n = x.shape[0]
-        dev = x.device
-        y = torch.empty((n, 64, 8, 8), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
-        L.check(L.load().bb_conv_in_forward(_p(x), _p(weight), _w_layout(weight), n, _p(y), _s(dev)),
-                "bb_conv_in_forward")
-        ctx.save_for_backward(x, weight)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
-        dw = None
-        if ctx.needs_input_grad[1]:
-            n = x.shape[0]
-            dev = x.device
-            lib = L.load()
-            dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            ws = torch.empty((lib.bb_conv_in_workspace_bytes(n) + 3) // 4, dtype=torch.float32, device=dev)
-            dw = torch.empty_like(weight, dtype=torch.float32)
-            L.check(lib.bb_conv_in_wgrad(_p(x), _p(dy), n, _p(ws), _w_layout(dw), _p(dw), _s(dev)),
-                    "bb_conv_in_wgrad")
-        return None, dw
-
-
 def conv3x3_prep_multi(weights):
     """bb_conv3x3_prep of every weight in one launch (bb_conv3x3_prep_multi):
     [(forward image, data-gradient image)] per weight, bf16."""
@@ -540,9 +496,6 @@ def cast_multi(dir_: int, srcs, dsts, perms) -> None:
             "bb_cast_multi")
 
 
-RELU_BGRAD = os.environ.get("BB_RELU_BGRAD", "0") == "1"  # measured equal to torch's pair (1.861 vs 1.858 ms): off
-
-
 class LinearReLUFunction(torch.autograd.Function):
     """relu(F.linear(x, w, b)) for 2-D x with the ReLU in hipBLASLt's GEMM
     epilogue (torch._addmm_activation; one kernel instead of the GEMM and a
@@ -558,22 +511,8 @@ class LinearReLUFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, weight, y = ctx.saved_tensors
-        db = None
-        if (RELU_BGRAD and ctx.needs_input_grad[2] and y.dtype == torch.bfloat16 and y.dim() == 2
-                and y.shape[1] % 64 == 0 and y.is_contiguous()):
-            # threshold_backward and the bias-gradient sum in one pass (bb_relu_bias_grad)
-            gy = gy.to(torch.bfloat16).contiguous()
-            g = torch.empty_like(y)
-            db = torch.empty(y.shape[1], dtype=torch.bfloat16, device=y.device)
-            lib = L.load()
-            ws = torch.empty((lib.bb_relu_bias_grad_workspace_bytes(y.shape[0], y.shape[1]) + 3) // 4,
-                             dtype=torch.float32, device=y.device)
-            L.check(lib.bb_relu_bias_grad(_p(gy), _p(y), 1, y.shape[0], y.shape[1], _p(ws), _p(g), _p(db),
-                                          _s(y.device)),
-                    "bb_relu_bias_grad")
-        else:
-            g = torch.ops.aten.threshold_backward(gy, y, 0)
-            db = g.sum(0) if ctx.needs_input_grad[2] else None
+        g = torch.ops.aten.threshold_backward(gy, y, 0)
+        db = g.sum(0) if ctx.needs_input_grad[2] else None
         dx = g.mm(weight) if ctx.needs_input_grad[0] else None
         dw = g.t().mm(x) if ctx.needs_input_grad[1] else None
         return dx, dw, db

@@ -60,7 +60,7 @@ class Info(C.Structure):
     ]
 
 
-ABI_VERSION = 3  # include/bbvec.h BB_ABI_VERSION
+ABI_VERSION = 4  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -160,14 +160,9 @@ SIGNATURES = {
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),
     "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
     "bb_ppo_loss_backward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
-    "bb_conv_in_workspace_bytes": (C.c_int64, [_I32]),
-    "bb_conv_in_forward": (C.c_int, [_P, _P, _I32, _I32, _P, _P]),
-    "bb_conv_in_wgrad": (C.c_int, [_P, _P, _I32, _P, _I32, _P, _P]),
     "bb_adam_clip_workspace_bytes": (C.c_int64, [_I32, _P]),
     "bb_adam_clip_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double, _F,
                                     _P, _P, _P]),
-    "bb_relu_bias_grad_workspace_bytes": (C.c_int64, [_I32, _I32]),
-    "bb_relu_bias_grad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     "bb_cast_multi": (C.c_int, [_I32, _I32, _P, _P, _P, _P, _P, _P]),
 }
 

@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 3  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE */
+#define BB_ABI_VERSION 4  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
+                              4: bb_conv_in_* and bb_relu_bias_grad* removed */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -393,21 +394,6 @@ int bb_conv3x3_forward_stats(const void* d_x, const void* d_w, int32_t N, int32_
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
 
-/* The CNN's input layer (the first Conv2d, 1 + 3 = 4 -> 64 channels, 3x3,
- * padding 1, network.py:75-117) under bf16 autocast: x f32 NHWC
- * (channels_last) [N][8][8][4] and the f32 weight [64][4][3][3] (w_layout 0)
- * or [64][3][3][4] (w_layout 1) are rounded to bf16 in the kernel as autocast
- * casts them; accumulation f32; y = conv(x, w) without bias, bf16 NHWC
- * [N][8][8][64].  bb_conv_in_wgrad writes the f32 weight gradient (in
- * w_layout) for the output gradient dy (bf16 NHWC); d_ws is scratch of
- * bb_conv_in_workspace_bytes(N) bytes; deterministic.  x, y, dy 16-byte
- * aligned.  (No input gradient: the network input needs none.) */
-int64_t bb_conv_in_workspace_bytes(int32_t N);
-int bb_conv_in_forward(const float* d_x, const float* d_w, int32_t w_layout, int32_t N, void* d_y,
-                       void* stream);
-int bb_conv_in_wgrad(const float* d_x, const void* d_dy, int32_t N, float* d_ws, int32_t w_layout,
-                     float* d_dw, void* stream);
-
 /* The end of the PPO minibatch step (PPOAgent.update, ppo.py:400-401):
  * nn.utils.clip_grad_norm_(params, max_norm) followed by
  * torch.optim.Adam(lr, betas, eps).step() (weight decay 0, no amsgrad), over
@@ -427,17 +413,6 @@ int bb_adam_clip_step(int32_t num_tensors, float* const* h_param, float* const* 
                       float* const* h_exp_avg, float* const* h_exp_avg_sq, float* const* h_step,
                       const int64_t* h_numel, double lr, double beta1, double beta2, double eps,
                       float max_norm, double* d_ws, float* d_total_norm, void* stream);
-
-/* Backward of a bf16 nn.Linear -> nn.ReLU (network.py:89-117) above the GEMMs:
- * g = gy where y > 0 else 0 (torch threshold_backward on the ReLU output y)
- * and the Linear bias gradient db = sum over rows of g (f32 accumulation in a
- * fixed order, bf16 result as torch's bf16 sum).  gy, y, g: row-major
- * [rows][cols] bf16, 16-byte aligned, cols a multiple of 64; db [cols] bf16;
- * d_ws f32 scratch of bb_relu_bias_grad_workspace_bytes(rows, cols) bytes.
- * dtype must be 1 (bf16).  Two launches, no atomics (deterministic). */
-int64_t bb_relu_bias_grad_workspace_bytes(int32_t rows, int32_t cols);
-int bb_relu_bias_grad(const void* d_gy, const void* d_y, int32_t dtype, int32_t rows, int32_t cols,
-                      float* d_ws, void* d_g, void* d_db, void* stream);
 
 /* bf16 autocast's parameter casts for the CNN's nn.Linear layers
  * (network.py:89-117 under torch.autocast), all tensors in one launch: dir 0

@@ -16,10 +16,8 @@ for r in $(seq 1 ${REPS:-2}); do
     esac
     pm=1; ex=""; [ $v = noprep ] && { fa=1; fc=1; rf=1; pm=0; }
     [ $v = copyin ] && { fa=1; fc=1; rf=1; ex=--copy-inputs; }
-    rb=0; [ $v = rb ] && { fa=1; fc=1; rf=1; rb=1; }
-    ci=0; [ $v = convin ] && { fa=1; fc=1; rf=1; ci=1; }
     rg=1; [ $v = norg ] && { fa=1; fc=1; rf=1; rg=0; }
-    BB_RES_GRAD_FUSED=$rg BB_HIP_CONV_IN=$ci BB_RELU_BGRAD=$rb BB_FUSED_ADAM=$fa BB_FUSED_CASTS=$fc BB_RES_FUSED=$rf BB_PREP_MULTI=$pm timeout -k 10 200 python tools/bench_ppo.py --envs 8192 --update-steps 300 --autocast bf16 $ex > gpurun_out/${TAG}_${v}_$r.json 2>gpurun_out/${TAG}_${v}_$r.err || { tail -5 gpurun_out/${TAG}_${v}_$r.err; exit 1; }
+    BB_RES_GRAD_FUSED=$rg BB_FUSED_ADAM=$fa BB_FUSED_CASTS=$fc BB_RES_FUSED=$rf BB_PREP_MULTI=$pm timeout -k 10 200 python tools/bench_ppo.py --envs 8192 --update-steps 300 --autocast bf16 $ex > gpurun_out/${TAG}_${v}_$r.json 2>gpurun_out/${TAG}_${v}_$r.err || { tail -5 gpurun_out/${TAG}_${v}_$r.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/${TAG}_${v}_$r.json'));print('$v', $r, d['update_step_ms'])"
   done
 done
