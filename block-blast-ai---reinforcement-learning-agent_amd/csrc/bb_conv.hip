@@ -98,12 +98,20 @@ __global__ void __launch_bounds__(kThreads) conv_prep_multi_kernel(const PrepTab
 }
 
 // LDS image of pixel rows of C bf16 channels: 16-byte chunk c of row r sits at
-// chunk c ^ key(r), so 16 lanes reading one chunk of 16 consecutive rows hit
-// 16 different bank groups (256-B rows: key = r & 15; 128-B rows, two per bank
-// line: key = (r >> 1) & 7).
+// chunk c ^ key(r).  The B fragment of mfma_f32_16x16x32_bf16 puts pixel n of a
+// 16-pixel tile in lanes n + 16 hq, chunk 4 cb + hq; ds_read_b128 serves lanes in
+// groups {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} (and +32): each group reads
+// chunk parity hq & 1 = 0 for pixels n in {0-3, 12-15} and 1 for n in {4-11},
+// or the reverse.  The key leaves bit 0 of the chunk alone and XORs the row's
+// residue mod 8 into bits 1-3 (256-B rows) or (row & 1, row >> 1 & 3) into the
+// bank line half and bits 1-2 (128-B rows, two per bank line): both pixel sets
+// are 8 consecutive rows mod 8 under every tap shift, so the 16 lanes of a group
+// hit 16 different 16-byte bank quads (r03's key r & 15 conflicted on the odd
+// column shifts: 40% extra LDS cycles).  Zero rows sit at ROWS + (row mod 16),
+// which keeps the key of the row they replace.
 template <int C>
 __device__ __forceinline__ int fwd_key(int r) {
-  return C == 128 ? (r & 15) : ((r >> 1) & 7);
+  return C == 128 ? ((r & 7) << 1) : (((r >> 1) & 3) << 1);
 }
 
 // Direct global -> LDS copy of one 16-byte chunk per lane: lane L of the wave
@@ -504,10 +512,10 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
 // pixel tiles per k-step, ds_read_b128, the next k-step's issued before this
 // one's MFMAs) and runs CW / 16 x 4 x KS MFMAs, then stores 4 channels x 1
 // pixel per lane and tile (8 bytes).  One barrier per board.  The LDS address
-// of a B fragment is base[t][i] ^ (cb << 6): base holds the tap's shifted row
-// (or its zero row), the lane's chunk and the slot, and the 32-channel block cb
-// only flips chunk bits (row offsets are multiples of 128 bytes, slot offsets
-// of 2 KiB).
+// of a B fragment is (atab[t][lane].i + slot) ^ (cb << 6): the table holds the
+// tap's shifted row (or its zero row) and the lane's chunk, and the 32-channel
+// block cb only flips chunk bits (row offsets are multiples of 128 bytes, slot
+// offsets of 2 KiB).
 // ---------------------------------------------------------------------------
 constexpr int kWsBuf = 3;
 #ifndef BB_CONV_WS_WAIT
@@ -541,6 +549,7 @@ conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
   constexpr int LPW = 64 * NCH / 256;               // direct copies per lane per board
   static_assert(NT >= 1 && LPW >= 1, "shape");
   __shared__ __attribute__((aligned(16))) uint8_t sm[kWsBuf * SLOT];
+  __shared__ int4 atab[9 * 64];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -574,17 +583,20 @@ conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
     const int s = i / (kWsZero * NCH), j = i % (kWsZero * NCH);
     *reinterpret_cast<uint4*>(sm + s * SLOT + 64 * RB + j * 16) = make_uint4(0, 0, 0, 0);
   }
-  // base[t][i]: byte address in slot 0 of chunk (hq ^ key) of the row that pixel 16 i + r16 reads at tap t
-  int base[9][4];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
+  // atab[t][lane].i: byte address in slot 0 of chunk (hq ^ key) of the row that pixel 16 i + r16 reads at tap t
+  // (the same for every wave; read one tap ahead, 4 VGPRs instead of 36 live addresses)
+  for (int e = tid; e < 9 * 64; e += 256) {
+    const int t = e / 64, l = e % 64, n = l & 15, q = l >> 4;
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    int a[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int dy = t / 3 - 1, dx = t % 3 - 1;
-      const int p = 16 * i + r16, yy = (p >> 3) + dy, xc = (p & 7) + dx;
+      const int p = 16 * i + n, yy = (p >> 3) + dy, xc = (p & 7) + dx;
       const int row = ((unsigned)yy < 8u && (unsigned)xc < 8u) ? yy * 8 + xc : 64 + ((p + 8 * dy + dx) & 15);
-      base[t][i] = row * RB + ((hq ^ fwd_key<CIN>(row)) << 4);
+      a[i] = row * RB + ((q ^ fwd_key<CIN>(row)) << 4);
     }
+    atab[e] = make_int4(a[0], a[1], a[2], a[3]);
+  }
   // board 0's copies have landed (the weight fragments and board 1's copies are younger and may be in flight:
   // the compiler waits for each fragment before its first use)
 #if BB_CONV_WS_WAIT
@@ -599,6 +611,7 @@ conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
     // board b + 2 G into the slot board b - G used (every wave passed the barrier after reading it)
     const int s2 = slot == 0 ? 2 : slot - 1;
     copy_board(b + 2 * G, s2);
+    const int so = slot * SLOT;
     uint2 ra[NT][4];
     if (radd) {  // block-uniform
 #pragma unroll
@@ -613,15 +626,21 @@ conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int4 ad[2];
+    ad[0] = atab[lane];
     bf16x8 bfr[2][4];
     auto load = [&](int s, int set) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        bfr[set][i] = *reinterpret_cast<const bf16x8*>(sm + (base[s / NCB][i] ^ ((s % NCB) << 6)));
+      const int4 a = ad[(s / NCB) & 1];
+      const int x = (s % NCB) << 6;
+      bfr[set][0] = *reinterpret_cast<const bf16x8*>(sm + ((a.x + so) ^ x));
+      bfr[set][1] = *reinterpret_cast<const bf16x8*>(sm + ((a.y + so) ^ x));
+      bfr[set][2] = *reinterpret_cast<const bf16x8*>(sm + ((a.z + so) ^ x));
+      bfr[set][3] = *reinterpret_cast<const bf16x8*>(sm + ((a.w + so) ^ x));
     };
     load(0, 0);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
+      if (s % NCB == 0 && s / NCB + 1 < 9) ad[(s / NCB + 1) & 1] = atab[(s / NCB + 1) * 64 + lane];
       if (s + 1 < KS) load(s + 1, (s + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -648,11 +667,6 @@ conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
     // loads, when present, already drained everything older)
     BB_WAIT_VM(LPW + 4 * NT);
     raw_barrier();
-    const int delta = slot == kWsBuf - 1 ? -(kWsBuf - 1) * SLOT : SLOT;
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) base[t][i] += delta;
     slot = slot == kWsBuf - 1 ? 0 : slot + 1;
   }
   BB_WAIT_VM(0);  // no copy into this workgroup's LDS may outlive it

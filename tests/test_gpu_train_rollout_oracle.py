@@ -17,8 +17,13 @@ be identical.
 * config 5 (one GPU's shard): 131,072 envs, long_train.yaml's horizon
   (T = 128), bf16 autocast, the rollout step captured in a HIP graph -- the
   eager warm-up collect, the capture + first replay, and a second replay, each
-  checked against the oracle continuing from the previous one.
+  checked against the oracle continuing from the previous one; then one bf16
+  update epoch over that buffer (16,777,216 samples: 8,192 graph-replayed
+  optimizer steps of the per-GPU minibatch 2,048, ppo.py:330-423) whose metrics
+  must be finite with a positive entropy; its time is printed.
 """
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -86,5 +91,16 @@ def test_config5_graph_rollout_matches_c_oracle(cuda):
         roll.collect(agent, graph=True)
         assert (roll._graph is not None) == (k > 0)
         _check_collect(roll, cpu, f"config 5 {label}")
+    agent.config.num_epochs = 1
+    last = agent.values_device(roll.x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m = agent.update(roll.buffer, last)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert all(np.isfinite(v) for v in m.values()), m
+    assert m["entropy"] > 0
+    print(f"config 5 shard: one bf16 update epoch over 131,072 x 128 samples (8,192 optimizer steps) in {dt:.2f} s "
+          f"({dt / 8192 * 1e3:.3f} ms per step), metrics {m}")
     roll.close()
     cpu.close()
