@@ -171,6 +171,9 @@ constexpr int kZeroRows = 16;
 #ifndef BB_CONV_FWD_SCI
 #define BB_CONV_FWD_SCI 64
 #endif
+#ifndef BB_CONV_FWD_UNROLL
+#define BB_CONV_FWD_UNROLL 1  // conv_fwd_kernel's stage loop unrolled with precomputed operand bases (0: rolled)
+#endif
 #ifndef BB_CONV_MFMA16
 #define BB_CONV_MFMA16 1  // forward tiles on mfma_f32_16x16x32_bf16 (0: 32x32x16)
 #endif
@@ -283,6 +286,59 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[j][i][e] = 0.f;
 
+#if BB_CONV_FWD_UNROLL
+  // every stage unrolled: tap, channel block and ring slot are compile-time, so an operand address is one
+  // precomputed per-lane base XOR a constant (the swizzle keys only flip chunk bits that the k offset does not
+  // carry, see fwd_key) and the ring slot rides in the ds_read offset
+  int aq[TN16], bq[TM16];
+#pragma unroll
+  for (int j = 0; j < TN16; ++j) aq[j] = abase[j] + ((hq ^ akey[j]) << 4);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    if (st + DIST < NS) stage_w(st + DIST);  // its slot was last read in stage st-1, before the barrier
+    const int cb = st % NCB;
+    if (cb == 0) {
+      const int t = st / NCB, dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < TM16; ++i) {
+        const int px = px0 + 16 * i + r16;
+        const int p = px & 63, yy = (p >> 3) + dy, xc = (p & 7) + dx;
+        const int row = ((unsigned)yy < 8u && (unsigned)xc < 8u) ? (px & ~63) + yy * 8 + xc
+                                                                  : ROWS + ((px + 8 * dy + dx) & 15);
+        bq[i] = row * RB + ((hq ^ fwd_key<CIN>(row)) << 4);
+      }
+    }
+    const int woff = XBYTES + (st % kFwdRing) * WBYTES;
+    bf16x8 afr[2][TN16], bfr[2][TM16];
+    auto load = [&](int kk, int set) {
+#pragma unroll
+      for (int j = 0; j < TN16; ++j)
+        afr[set][j] = *reinterpret_cast<const bf16x8*>(sm + woff + (aq[j] ^ (kk << 6)));
+#pragma unroll
+      for (int i = 0; i < TM16; ++i)
+        bfr[set][i] = *reinterpret_cast<const bf16x8*>(xs + (bq[i] ^ ((cb * (SCI / 8) + 4 * kk) << 4)));
+    };
+    load(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < KK16; ++kk) {
+      if (kk + 1 < KK16) load(kk + 1, (kk + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < TN16; ++j)
+#pragma unroll
+        for (int i = 0; i < TM16; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[kk & 1][j], bfr[kk & 1][i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int after = min(NS, st + DIST + 1) - (st + 2);
+    if (after >= 4) BB_WAIT_VM(4 * GPW);
+    else if (after == 3) BB_WAIT_VM(3 * GPW);
+    else if (after == 2) BB_WAIT_VM(2 * GPW);
+    else if (after == 1) BB_WAIT_VM(GPW);
+    else BB_WAIT_VM(0);
+    raw_barrier();
+  }
+#else
   int rb[TM16], key[TM16];
   for (int st = 0; st < NS; ++st) {
     if (st + DIST < NS) stage_w(st + DIST);  // its slot was last read in stage st-1, before the barrier
@@ -329,6 +385,7 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
     else BB_WAIT_VM(0);
     raw_barrier();
   }
+#endif
 #if BB_CONV_STORE_LDS
   // the output tile goes through LDS (free after the last stage's barrier) so that every global
   // store is a whole 16-byte chunk of a pixel row: row px of COUT bf16, 16-byte chunk c at c ^ (px & 15)
@@ -518,6 +575,10 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
 // offsets of 2 KiB).
 // ---------------------------------------------------------------------------
 constexpr int kWsBuf = 3;
+#ifndef BB_CONV_WS_PF
+#define BB_CONV_WS_PF 2  // k-steps of B-fragment prefetch in conv_fwd_ws_kernel
+#endif
+constexpr int kWsPf = BB_CONV_WS_PF;
 #ifndef BB_CONV_WS_WAIT
 #define BB_CONV_WS_WAIT 0
 #endif
@@ -626,28 +687,33 @@ conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int4 ad[2];
+    // B fragments read kWsPf k-steps ahead (one wave per SIMD: nothing else hides the LDS latency)
+    constexpr int PF = kWsPf;
+    int4 ad[3];
     ad[0] = atab[lane];
-    bf16x8 bfr[2][4];
-    auto load = [&](int s, int set) {
-      const int4 a = ad[(s / NCB) & 1];
+    ad[1] = atab[64 + lane];
+    bf16x8 bfr[PF + 1][4];
+    auto load = [&](int s) {
+      const int4 a = ad[(s / NCB) % 3];
       const int x = (s % NCB) << 6;
-      bfr[set][0] = *reinterpret_cast<const bf16x8*>(sm + ((a.x + so) ^ x));
-      bfr[set][1] = *reinterpret_cast<const bf16x8*>(sm + ((a.y + so) ^ x));
-      bfr[set][2] = *reinterpret_cast<const bf16x8*>(sm + ((a.z + so) ^ x));
-      bfr[set][3] = *reinterpret_cast<const bf16x8*>(sm + ((a.w + so) ^ x));
+      bf16x8* d = bfr[s % (PF + 1)];
+      d[0] = *reinterpret_cast<const bf16x8*>(sm + ((a.x + so) ^ x));
+      d[1] = *reinterpret_cast<const bf16x8*>(sm + ((a.y + so) ^ x));
+      d[2] = *reinterpret_cast<const bf16x8*>(sm + ((a.z + so) ^ x));
+      d[3] = *reinterpret_cast<const bf16x8*>(sm + ((a.w + so) ^ x));
     };
-    load(0, 0);
+#pragma unroll
+    for (int s = 0; s < PF; ++s) load(s);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      if (s % NCB == 0 && s / NCB + 1 < 9) ad[(s / NCB + 1) & 1] = atab[(s / NCB + 1) * 64 + lane];
-      if (s + 1 < KS) load(s + 1, (s + 1) & 1);
+      if (s % NCB == 0 && s / NCB + 2 < 9) ad[(s / NCB + 2) % 3] = atab[(s / NCB + 2) * 64 + lane];
+      if (s + PF < KS) load(s + PF);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][s], bfr[s & 1][i], acc[j][i], 0, 0, 0);
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][s], bfr[s % (PF + 1)][i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     // lane holds D[co0 + 16 j + 4 hq + reg][16 i + r16]

@@ -309,29 +309,6 @@ def test_update_direct_gather_equals_copies(cuda, monkeypatch):
         assert torch.allclose(a, b, rtol=1e-3, atol=1e-5)
 
 
-@pytest.mark.parametrize("rows,cols", [(2048, 512), (2048, 256), (2048, 128), (37, 64)])
-def test_relu_bias_grad(cuda, rows, cols):
-    """bb_relu_bias_grad: g == threshold_backward(gy, y, 0) exactly; db == the
-    f32 column sums of g rounded to bf16 (torch's bf16 sum), within one bf16
-    rounding of torch's own sum order."""
-    from runtime import kernels as K
-
-    g0 = torch.Generator(device=cuda).manual_seed(rows + cols)
-    gy = torch.randn((rows, cols), device=cuda, generator=g0).to(torch.bfloat16)
-    y = torch.relu(torch.randn((rows, cols), device=cuda, generator=g0)).to(torch.bfloat16)
-    y[0, :8] = torch.tensor([0.0, -0.0, float("nan"), 1.0, 0.0, 2.0, 0.0, 3.0], device=cuda).to(torch.bfloat16)
-    g = torch.empty_like(y)
-    db = torch.empty(cols, dtype=torch.bfloat16, device=cuda)
-    lib = K.L.load()
-    ws = torch.empty(lib.bb_relu_bias_grad_workspace_bytes(rows, cols) // 4, dtype=torch.float32, device=cuda)
-    assert lib.bb_relu_bias_grad(K._p(gy), K._p(y), 1, rows, cols, K._p(ws), K._p(g), K._p(db), K._s(cuda)) == 0
-    want = torch.ops.aten.threshold_backward(gy, y, 0)
-    assert torch.equal(g.view(torch.int16), want.view(torch.int16))
-    assert torch.allclose(db.float(), want.float().sum(0), rtol=8e-3, atol=1e-2)
-    assert torch.allclose(db.float(), want.sum(0).float(), rtol=1.6e-2, atol=2e-2)
-    assert lib.bb_relu_bias_grad(K._p(gy), K._p(y), 1, rows, 48, K._p(ws), K._p(g), K._p(db), K._s(cuda)) != 0
-
-
 def test_network_res_grad_fused_equals_unfused(cuda, monkeypatch):
     """The identity path's input gradient added in conv1's data-gradient store
     pass (bb_conv3x3_forward_add) == autograd's separate add, bit for bit, for
