@@ -11,4 +11,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/${TAG}_pytest.log
 [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_profile.sh "$TAG"
-ARGS="--mode step --steps 2000 --warmup 100" PMC_ARGS="--kernels rollout_kernel --steps-per-launch 1" bash tools/gpu_profile.sh "${TAG}_step"
+ARGS="--mode step --steps 2000 --warmup 100" PMC_ARGS="--kernels step_fused_kernel --steps-per-launch 1" bash tools/gpu_profile.sh "${TAG}_step"
