@@ -666,26 +666,6 @@ extern "C" int bb_bn_forward_res(const void* d_x, const void* d_res, int32_t dty
                          d_y, stream, "bb_bn_forward_res");
 }
 
-extern "C" int bb_bn_forward_parts(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N,
-                                   int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
-                                   const float* d_bias, float eps, int32_t relu, double* d_ws, const double* d_part,
-                                   int32_t nparts, float* d_save_mean, float* d_save_invstd, float* d_running_mean,
-                                   float* d_running_var, float momentum, int64_t* d_num_batches_tracked, void* d_y,
-                                   void* stream) {
-  int rc = bn_check(dtype, nhwc, N, C, HW);
-  if (rc != BB_OK) return rc;
-  if (!d_x || !d_weight || !d_bias || !d_ws || !d_part || !d_save_mean || !d_save_invstd || !d_y || nparts <= 0)
-    return fail(nullptr, BB_ERR_ARG, "bb_bn_forward_parts: NULL argument or no partials");
-  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
-  if (d_res && reinterpret_cast<uintptr_t>(d_res) % 16 != 0)
-    return fail(nullptr, BB_ERR_ARG, "bb_bn: d_res must be 16-byte aligned");
-  hipError_t st = launch_bn_forward_parts(d_x, d_res, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu,
-                                          d_ws, d_part, nparts, d_save_mean, d_save_invstd, d_running_mean,
-                                          d_running_var, momentum, d_num_batches_tracked, d_y, (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_forward_parts");
-  return BB_OK;
-}
-
 extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N, int32_t C,
                               int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias,
                               const float* d_save_mean, const float* d_save_invstd, int32_t relu, double* d_ws,
@@ -788,25 +768,6 @@ extern "C" int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, i
     return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward: tensors must be 16-byte aligned");
   hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward");
-  return BB_OK;
-}
-
-extern "C" int64_t bb_conv3x3_stats_parts(int32_t N, int32_t cout) {
-  if (N <= 0 || (cout != 64 && cout != 128)) return -1;
-  return conv3x3_stats_parts(N, cout);
-}
-
-extern "C" int bb_conv3x3_forward_stats(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout,
-                                        void* d_y, const float* d_pre_bias, double* d_part, void* stream) {
-  int rc = conv_check(N, cin, cout, "bb_conv3x3_forward_stats");
-  if (rc != BB_OK) return rc;
-  if (!d_x || !d_w || !d_y || !d_part) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: NULL argument");
-  if (!al16(d_x) || !al16(d_w) || !al16(d_y))
-    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: tensors must be 16-byte aligned");
-  hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream, nullptr, d_pre_bias, d_part);
-  if (st == hipErrorInvalidValue)
-    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: not available in this (variant) build");
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward_stats");
   return BB_OK;
 }
 

@@ -201,16 +201,11 @@ __device__ __forceinline__ uint32_t add2_bf16(uint32_t a, uint32_t b) {  // two 
 // radd (NULL = none, shipped LDS-staged store path only): y = bf16(conv) + radd, rounded again -- the
 // data gradient of a ResidualBlock's first convolution plus the identity path's gradient, as autograd's
 // separate add kernel computed it
-// part (NULL = none, shipped LDS-staged store path only): the BatchNorm forward statistics of the output --
-// per channel c, over this block's pixels, the fp64 sums of u = y + pre_bias[c] and u^2, with y the stored
-// bf16 value (bb_nn.hip's reduction pass reads the same values) -- written to part[block][c][3] (third 0)
 template <int CIN, int COUT>
 __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ y, int nb,
-                                                               const uint16_t* __restrict__ radd,
-                                                               const float* __restrict__ pb,
-                                                               double* __restrict__ part) {
+                                                               const uint16_t* __restrict__ radd) {
   constexpr int RB = CIN * 2;                 // bytes per pixel row
   constexpr int NCH = CIN / 8;                // 16-byte chunks per pixel row
   constexpr int FB = fwd_boards<COUT>();
@@ -415,38 +410,6 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
       v = make_uint4(add2_bf16(v.x, a.x), add2_bf16(v.y, a.y), add2_bf16(v.z, a.z), add2_bf16(v.w, a.w));
     }
     *reinterpret_cast<uint4*>(y + o) = v;
-  }
-  if (part) {  // block-uniform
-    // thread t: channel t % COUT over pixels t / COUT, + TPC, ... (ascending), then the TPC partial sums of a
-    // channel added in thread order: a fixed order, so the statistics are deterministic
-    constexpr int TPC = kFwdThreads / COUT;
-    __shared__ double red[2][kFwdThreads];
-    const int c = tid % COUT;
-    const float pbc = pb ? pb[c] : 0.f;
-    const int vrows = min(ROWS, (nb - b0) * 64);
-    double sa = 0.0, qa = 0.0;
-    for (int px = tid / COUT; px < vrows; px += TPC) {
-      const uint32_t v = *reinterpret_cast<const uint16_t*>(os + px * (COUT * 2) +
-                                                            (((c >> 3) ^ (px & 15 & (OCH - 1))) << 4) + (c & 7) * 2);
-      const double u = (double)(__uint_as_float(v << 16) + pbc);
-      sa += u;
-      qa += u * u;
-    }
-    red[0][tid] = sa;
-    red[1][tid] = qa;
-    __syncthreads();
-    if (tid < COUT) {
-      double S = 0.0, Q = 0.0;
-#pragma unroll
-      for (int k = 0; k < TPC; ++k) {
-        S += red[0][k * COUT + tid];
-        Q += red[1][k * COUT + tid];
-      }
-      double* o = part + ((size_t)blockIdx.x * COUT + tid) * 3;
-      o[0] = S;
-      o[1] = Q;
-      o[2] = 0.0;
-    }
   }
 #else
 #pragma unroll
@@ -1001,23 +964,21 @@ int wgrad_bpc(int nb, int nchunk) {
 }
 
 #ifndef BB_CONV_FWD_WS
-#define BB_CONV_FWD_WS 0  // 1: forward / data gradient on conv_fwd_ws_kernel (parity-green, first build 46.2 vs
-                          // 42.2 us per 128 -> 128 call: in work); the statistics epilogue always uses conv_fwd_kernel
+#define BB_CONV_FWD_WS 0  // 1: forward / data gradient on conv_fwd_ws_kernel (parity-green, 46-48 vs 39.5 us per
+                          // 128 -> 128 call)
 #endif
 
 template <int CIN, int COUT>
-hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr,
-                 const float* pb = nullptr, double* part = nullptr) {
+hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr) {
   if (nb <= 0) return hipErrorInvalidValue;
-  if (BB_CONV_FWD_WS && !part) {
+  if (BB_CONV_FWD_WS) {
     hipLaunchKernelGGL((conv_fwd_ws_kernel<CIN, COUT>), dim3(ws_grid(nb)), dim3(256), 0, s, (const uint16_t*)x,
                        (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd);
     return hipGetLastError();
   }
-  if ((radd || part) && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS))
-    return hipErrorInvalidValue;  // variant builds: no fused add / statistics
+  if (radd && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS)) return hipErrorInvalidValue;  // variant builds: no fused add
   hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>()), dim3(kFwdThreads), 0, s,
-                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd, pb, part);
+                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd);
   return hipGetLastError();
 }
 
@@ -1079,16 +1040,11 @@ hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int
 }
 
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
-                                  const void* radd, const float* pb, double* part) {
-  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s, radd, pb, part);
-  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd, pb, part);
-  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd, pb, part);
-  return fwd_t<128, 128>(x, w, nb, y, s, radd, pb, part);
-}
-
-int conv3x3_stats_parts(int nb, int cout) {
-  const int fb = cout == 128 ? fwd_boards<128>() : fwd_boards<64>();
-  return (nb + fb - 1) / fb;
+                                  const void* radd) {
+  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s, radd);
+  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd);
+  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd);
+  return fwd_t<128, 128>(x, w, nb, y, s, radd);
 }
 
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,

@@ -117,12 +117,7 @@ hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* 
 hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
                                      const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s);
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
-                                  const void* radd = nullptr, const float* pb = nullptr, double* part = nullptr);
-int conv3x3_stats_parts(int nb, int cout);
-hipError_t launch_bn_forward_parts(const void* x, const void* res, int dtype, int nhwc, int N, int C, int HW,
-                                   const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
-                                   const double* part, int nparts, float* save_mean, float* save_invstd,
-                                   float* rmean, float* rvar, float momentum, int64_t* nbt, void* y, hipStream_t s);
+                                  const void* radd = nullptr);
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);
 

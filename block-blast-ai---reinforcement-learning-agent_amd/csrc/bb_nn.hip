@@ -457,27 +457,6 @@ hipError_t bn_forward_t(const void* x, const void* res, int nhwc, int N, int C, 
   return hipGetLastError();
 }
 
-// bn_forward_t without the reduction pass: the block partials part[nparts][C][kQ] came from the preceding
-// convolution's epilogue (bb_conv3x3_forward_stats)
-template <typename T>
-hipError_t bn_forward_parts_t(const void* x, const void* res, int nhwc, int N, int C, int HW, const float* pb,
-                              const float* w, const float* b, float eps, int relu, double* ws, const double* part,
-                              int nparts, float* save_mean, float* save_invstd, float* rmean, float* rvar,
-                              float momentum, int64_t* nbt, void* y, hipStream_t s) {
-  const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
-  const Ws k = split_ws(ws, C);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, part, nparts, C, (double)N * HW,
-                     eps, pb, w, b, save_mean, save_invstd, rmean, rvar, momentum, nbt, k.coef);
-  const dim3 ge(grid_for_elems(p.chunks, nhwc));
-  if (nhwc)
-    hipLaunchKernelGGL((bn_apply_fwd<T, true>), ge, dim3(kBnThreads), 0, s, x, res, y, p.chunks, C, p.cpr, relu,
-                       k.coef);
-  else
-    hipLaunchKernelGGL((bn_apply_fwd<T, false>), ge, dim3(kBnThreads), 0, s, x, res, y, p.chunks, C, p.cpr, relu,
-                       k.coef);
-  return hipGetLastError();
-}
-
 template <typename T>
 hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, int HW, const float* pb,
                          const float* w, const float* b, const float* mean, const float* invstd, int relu, double* ws,
@@ -513,17 +492,6 @@ hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc
                                         rvar, momentum, nbt, y, s);
   return bn_forward_t<float>(x, res, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar, momentum,
                              nbt, y, s);
-}
-
-hipError_t launch_bn_forward_parts(const void* x, const void* res, int dtype, int nhwc, int N, int C, int HW,
-                                   const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
-                                   const double* part, int nparts, float* save_mean, float* save_invstd,
-                                   float* rmean, float* rvar, float momentum, int64_t* nbt, void* y, hipStream_t s) {
-  if (dtype == 1)
-    return bn_forward_parts_t<__hip_bfloat16>(x, res, nhwc, N, C, HW, pb, w, b, eps, relu, ws, part, nparts,
-                                              save_mean, save_invstd, rmean, rvar, momentum, nbt, y, s);
-  return bn_forward_parts_t<float>(x, res, nhwc, N, C, HW, pb, w, b, eps, relu, ws, part, nparts, save_mean,
-                                   save_invstd, rmean, rvar, momentum, nbt, y, s);
 }
 
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,

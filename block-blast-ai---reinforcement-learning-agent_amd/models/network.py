@@ -41,16 +41,15 @@ class BatchNorm2d(nn.BatchNorm2d):
 
         return bn_fusable(x)
 
-    def forward(self, x: torch.Tensor, pre_bias: Optional[torch.Tensor] = None, parts=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, pre_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
         """BatchNorm2d(x + pre_bias) [-> ReLU]; ``pre_bias`` is a preceding
-        convolution's bias that was left out of the convolution; ``parts`` its
-        statistics from the convolution's epilogue (conv_nobias_stats)."""
+        convolution's bias that was left out of the convolution."""
         if self.fusable(x):
             from runtime.kernels import BatchNormReLUFunction
 
             return BatchNormReLUFunction.apply(x, pre_bias, self.weight, self.bias, self.running_mean,
                                                self.running_var, self.momentum, self.eps, self.fuse_relu,
-                                               self.num_batches_tracked, parts)  # += 1 in the finalize kernel
+                                               self.num_batches_tracked)  # += 1 in the finalize kernel
         if pre_bias is not None:
             x = x + pre_bias.view(1, -1, 1, 1).to(x.dtype)
         y = super().forward(x)
@@ -66,9 +65,6 @@ PREP_MULTI = os.environ.get("BB_PREP_MULTI", "1") != "0"  # the HIP convs' weigh
 RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass
 # ... and the identity path's input gradient added in conv1's data-gradient store pass (no add kernel)
 RES_GRAD_FUSED = os.environ.get("BB_RES_GRAD_FUSED", "1") != "0"
-# the BatchNorm forward statistics of a HIP convolution's output summed in its epilogue (no reduction pass):
-# parity-tested, measured slower and opt-in (bf16 update step 1.851 vs 1.840 ms, profiles/r03/bns/)
-CONV_BN_STATS = os.environ.get("BB_CONV_BN_STATS", "0") == "1"
 
 
 def _hip_conv_on(x: torch.Tensor) -> bool:
@@ -90,33 +86,15 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> 
     return conv._conv_forward(x, conv.weight, None)
 
 
-def conv_nobias_stats(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None, mailbox=None):
-    """conv_nobias, and where the convolution runs on the HIP kernels and feeds a
-    fused BatchNorm, the BatchNorm's forward statistics of conv(x) + conv.bias
-    from the convolution's epilogue (bb_conv3x3_forward_stats): (z, parts or None)."""
-    if CONV_BN_STATS and isinstance(bn, BatchNorm2d) and bn.use_fused and bn.training and _hip_conv_on(x):
-        from runtime import lib as L
-        from runtime.kernels import Conv3x3Function, conv3x3_fusable
-
-        if conv3x3_fusable(x, conv):
-            nparts = L.load().bb_conv3x3_stats_parts(x.shape[0], conv.out_channels)
-            parts = torch.empty((nparts, conv.out_channels, 3), dtype=torch.float64, device=x.device)
-            z = Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox,
-                                      (conv.bias, parts))
-            return z, parts
-    return conv_nobias(conv, x, images, mailbox), None
-
-
 def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None, mailbox=None) -> torch.Tensor:
     """bn(conv(x)).  When the BatchNorm runs on the HIP kernels the
     convolution's bias is added inside them (one add on load instead of a
     separate pass, and its gradient comes out of the BatchNorm backward instead
-    of a reduction over dy); after a HIP convolution its statistics come from
-    the convolution's epilogue."""
+    of a reduction over dy)."""
     if isinstance(bn, BatchNorm2d) and conv.bias is not None and bn.training and x.is_cuda and bn.use_fused:
-        z, parts = conv_nobias_stats(conv, bn, x, images, mailbox)
+        z = conv_nobias(conv, x, images, mailbox)
         if bn.fusable(z):
-            return bn(z, pre_bias=conv.bias, parts=parts)
+            return bn(z, pre_bias=conv.bias)
         return bn(z + conv.bias.view(1, -1, 1, 1).to(z.dtype))
     return bn(conv(x))
 
@@ -163,16 +141,16 @@ class ResidualBlock(nn.Module):
                 mailbox = GradMailbox()
         y = conv_bn(self.conv1, self.bn1, x, images, mailbox)
         if fused:
-            z, parts = conv_nobias_stats(conv2, bn2, y, images)
+            z = conv_nobias(conv2, y, images)
             from runtime.kernels import BatchNormAddReLUFunction, _bn_layout
 
             if bn2.fusable(z) and x.dtype == z.dtype and x.shape == z.shape and _bn_layout(x) == _bn_layout(z):
                 # bn2 -> + identity -> relu in the BatchNorm apply pass
                 return BatchNormAddReLUFunction.apply(z, conv2.bias, x, bn2.weight, bn2.bias, bn2.running_mean,
                                                       bn2.running_var, bn2.momentum, bn2.eps,
-                                                      bn2.num_batches_tracked, mailbox, parts)
+                                                      bn2.num_batches_tracked, mailbox)
             # (an unused mailbox stays empty: conv1's data gradient is then the plain one, and autograd adds)
-            return F.relu(bn2(z, pre_bias=conv2.bias, parts=parts) + x)
+            return F.relu(bn2(z, pre_bias=conv2.bias) + x)
         y = conv_bn(conv2, bn2, y, images)
         return F.relu(y + x)
 

@@ -170,7 +170,7 @@ class BatchNormReLUFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, pre_bias, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool,
-                num_batches_tracked=None, parts=None):
+                num_batches_tracked=None):
         nhwc = _bn_layout(x)
         x = x.contiguous(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         n, c, h, w = x.shape
@@ -179,19 +179,11 @@ class BatchNormReLUFunction(torch.autograd.Function):
         ws = _bn_workspace(x, nhwc)
         mean = torch.empty(c, dtype=torch.float32, device=dev)
         invstd = torch.empty(c, dtype=torch.float32, device=dev)
-        if parts is not None:  # the statistics came from the convolution's epilogue (conv_bn)
-            L.check(L.load().bb_bn_forward_parts(_p(x), None, _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias),
-                                                 _p(weight), _p(bias), float(eps), int(relu), _p(ws), _p(parts),
-                                                 parts.shape[0], _p(mean), _p(invstd), _p(running_mean),
-                                                 _p(running_var), float(momentum), _p(num_batches_tracked), _p(y),
-                                                 _s(dev)),
-                    "bb_bn_forward_parts")
-        else:
-            L.check(L.load().bb_bn_forward(_p(x), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight),
-                                           _p(bias), float(eps), int(relu), _p(ws), _p(mean), _p(invstd),
-                                           _p(running_mean), _p(running_var), float(momentum),
-                                           _p(num_batches_tracked), _p(y), _s(dev)),
-                    "bb_bn_forward")
+        L.check(L.load().bb_bn_forward(_p(x), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight),
+                                       _p(bias), float(eps), int(relu), _p(ws), _p(mean), _p(invstd),
+                                       _p(running_mean), _p(running_var), float(momentum),
+                                       _p(num_batches_tracked), _p(y), _s(dev)),
+                "bb_bn_forward")
         ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd)
         ctx.relu = bool(relu)
         ctx.nhwc = nhwc
@@ -213,7 +205,7 @@ class BatchNormReLUFunction(torch.autograd.Function):
                                         _p(weight), _p(bias), _p(mean), _p(invstd), int(ctx.relu), _p(ws), _p(dx),
                                         _p(dw), _p(db), _p(dpb), _s(dev)),
                 "bb_bn_backward")
-        return dx, dpb, dw, db, None, None, None, None, None, None, None
+        return dx, dpb, dw, db, None, None, None, None, None, None
 
 
 class BatchNormAddReLUFunction(torch.autograd.Function):
@@ -226,7 +218,7 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, pre_bias, res, weight, bias, running_mean, running_var, momentum: float, eps: float,
-                num_batches_tracked=None, grad_mailbox=None, parts=None):
+                num_batches_tracked=None, grad_mailbox=None):
         ctx.mailbox = grad_mailbox
         nhwc = _bn_layout(x)
         fmt = torch.channels_last if nhwc else torch.contiguous_format
@@ -238,19 +230,11 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
         ws = _bn_workspace(x, nhwc)
         mean = torch.empty(c, dtype=torch.float32, device=dev)
         invstd = torch.empty(c, dtype=torch.float32, device=dev)
-        if parts is not None:  # the statistics came from the convolution's epilogue
-            L.check(L.load().bb_bn_forward_parts(_p(x), _p(res), _BN_DTYPES[x.dtype], nhwc, n, c, h * w,
-                                                 _p(pre_bias), _p(weight), _p(bias), float(eps), 1, _p(ws),
-                                                 _p(parts), parts.shape[0], _p(mean), _p(invstd),
-                                                 _p(running_mean), _p(running_var), float(momentum),
-                                                 _p(num_batches_tracked), _p(y), _s(dev)),
-                    "bb_bn_forward_parts")
-        else:
-            L.check(L.load().bb_bn_forward_res(_p(x), _p(res), _BN_DTYPES[x.dtype], nhwc, n, c, h * w,
-                                               _p(pre_bias), _p(weight), _p(bias), float(eps), 1, _p(ws), _p(mean),
-                                               _p(invstd), _p(running_mean), _p(running_var), float(momentum),
-                                               _p(num_batches_tracked), _p(y), _s(dev)),
-                    "bb_bn_forward_res")
+        L.check(L.load().bb_bn_forward_res(_p(x), _p(res), _BN_DTYPES[x.dtype], nhwc, n, c, h * w,
+                                           _p(pre_bias), _p(weight), _p(bias), float(eps), 1, _p(ws), _p(mean),
+                                           _p(invstd), _p(running_mean), _p(running_var), float(momentum),
+                                           _p(num_batches_tracked), _p(y), _s(dev)),
+                "bb_bn_forward_res")
         ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd, y)
         ctx.nhwc = nhwc
         return y
@@ -275,7 +259,7 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
         if ctx.mailbox is not None and ctx.needs_input_grad[2]:
             ctx.mailbox.put(g)  # the block's first convolution adds it to its data gradient
             gres = None
-        return dx, dpb, gres, dw, db, None, None, None, None, None, None, None
+        return dx, dpb, gres, dw, db, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -308,7 +292,7 @@ class Conv3x3Function(torch.autograd.Function):
     kernel over dy with the tap-reversed, transposed weight image)."""
 
     @staticmethod
-    def forward(ctx, x, weight, images=None, grad_mailbox=None, stats=None):
+    def forward(ctx, x, weight, images=None, grad_mailbox=None):
         _need_cuda(x, weight)
         ctx.mailbox = grad_mailbox
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -324,12 +308,7 @@ class Conv3x3Function(torch.autograd.Function):
             wd = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
             L.check(lib.bb_conv3x3_prep(_p(weight), cin, cout, wl, _p(wf), _p(wd), _s(dev)), "bb_conv3x3_prep")
         y = torch.empty((n, cout, 8, 8), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
-        if stats is not None:  # (pre_bias, parts): the following BatchNorm's statistics in the epilogue
-            pre_bias, parts = stats
-            L.check(lib.bb_conv3x3_forward_stats(_p(x), _p(wf), n, cin, cout, _p(y), _p(pre_bias), _p(parts),
-                                                 _s(dev)), "bb_conv3x3_forward_stats")
-        else:
-            L.check(lib.bb_conv3x3_forward(_p(x), _p(wf), n, cin, cout, _p(y), _s(dev)), "bb_conv3x3_forward")
+        L.check(lib.bb_conv3x3_forward(_p(x), _p(wf), n, cin, cout, _p(y), _s(dev)), "bb_conv3x3_forward")
         ctx.save_for_backward(x, wd, weight)
         return y
 
@@ -360,7 +339,7 @@ class Conv3x3Function(torch.autograd.Function):
             dw = torch.empty_like(weight, dtype=torch.float32)
             L.check(lib.bb_conv3x3_wgrad(_p(x), _p(dy), n, cin, cout, _p(ws), _w_layout(dw), _p(dw), _s(dev)),
                     "bb_conv3x3_wgrad")
-        return dx, dw, None, None, None
+        return dx, dw, None, None
 
 
 class GradMailbox:

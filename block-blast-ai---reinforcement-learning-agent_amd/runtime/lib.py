@@ -60,7 +60,7 @@ class Info(C.Structure):
     ]
 
 
-ABI_VERSION = 4  # include/bbvec.h BB_ABI_VERSION
+ABI_VERSION = 5  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -145,8 +145,6 @@ SIGNATURES = {
                                 _P]),
     "bb_bn_forward_res": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P,
                                     _F, _P, _P, _P]),
-    "bb_bn_forward_parts": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _I32, _P,
-                                      _P, _P, _P, _F, _P, _P, _P]),
     "bb_bn_backward": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                  _P]),
     "bb_conv3x3_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
@@ -154,8 +152,6 @@ SIGNATURES = {
     "bb_conv3x3_prep_multi": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P]),
     "bb_conv3x3_forward": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_conv3x3_forward_add": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
-    "bb_conv3x3_stats_parts": (C.c_int64, [_I32, _I32]),
-    "bb_conv3x3_forward_stats": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     "bb_conv3x3_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _P, _P]),
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),
     "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),

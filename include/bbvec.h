@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 4  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
-                              4: bb_conv_in_* and bb_relu_bias_grad* removed */
+#define BB_ABI_VERSION 5  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
+                              4: bb_conv_in_* and bb_relu_bias_grad* removed;
+                              5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -314,17 +315,6 @@ int bb_bn_forward_res(const void* d_x, const void* d_res, int32_t dtype, int32_t
                       const float* d_bias, float eps, int32_t relu, double* d_ws, float* d_save_mean,
                       float* d_save_invstd, float* d_running_mean, float* d_running_var, float momentum,
                       int64_t* d_num_batches_tracked, void* d_y, void* stream);
-/* bb_bn_forward / bb_bn_forward_res (d_res NULL or not) without the statistics pass: d_part holds the
- * per-channel fp64 sums of x + pre_bias and of its square in nparts block partials [nparts][C][3] (third
- * unused), as bb_conv3x3_forward_stats writes them for the convolution that produced x (conv_bn,
- * network.py:75-117 / ResidualBlock network.py:14-30: nn.Conv2d -> nn.BatchNorm2d).  Finalisation (mean,
- * inverse std, running statistics, num_batches_tracked) and the apply pass are bb_bn_forward's. */
-int bb_bn_forward_parts(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N,
-                        int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
-                        const float* d_bias, float eps, int32_t relu, double* d_ws, const double* d_part,
-                        int32_t nparts, float* d_save_mean, float* d_save_invstd, float* d_running_mean,
-                        float* d_running_var, float momentum, int64_t* d_num_batches_tracked, void* d_y,
-                        void* stream);
 int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N,
                    int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                    const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
@@ -384,13 +374,6 @@ int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin,
  * gradient folded in (network.py:14-30). */
 int bb_conv3x3_forward_add(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout,
                            const void* d_add, void* d_y, void* stream);
-/* bb_conv3x3_forward that also writes the BatchNorm forward statistics of y for the following
- * BatchNorm (bb_bn_forward_parts): per channel, the fp64 sums of u = y + d_pre_bias[c] (d_pre_bias: the
- * convolution's bias, NULL = 0) and of u^2 over each block's pixels, y being the stored bf16 value, into
- * d_part [bb_conv3x3_stats_parts(N, cout)][cout][3] doubles.  Fixed summation order: deterministic. */
-int64_t bb_conv3x3_stats_parts(int32_t N, int32_t cout);
-int bb_conv3x3_forward_stats(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
-                             const float* d_pre_bias, double* d_part, void* stream);
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
 

@@ -24,7 +24,7 @@ def test_header_and_binding_agree():
 def test_library_exports_every_symbol(lib):
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.bb_abi_version() == L.ABI_VERSION == 4
+    assert lib.bb_abi_version() == L.ABI_VERSION == 5
 
 
 def test_struct_sizes(lib):
