@@ -518,190 +518,6 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
 }
 
 // ---------------------------------------------------------------------------
-// forward / data gradient, weight-stationary (the shipped path without the
-// statistics epilogue).  conv_fwd_kernel streams the whole weight tensor from
-// L2 through LDS for every 2 boards (295 KB per 37.7 MFLOP at 128 -> 128:
-// ~300 MB of L2 reads per 2,048-board call, and a barrier per tap stage).
-// Here each workgroup is persistent (one per CU, one wave per SIMD) and holds
-// its weights in registers for all of its boards: wave w owns output channels
-// [w CW, (w + 1) CW), CW = COUT / 4, as mfma_f32_16x16x32_bf16 A fragments
-// (CW / 16 tiles x 9 CIN / 32 k-steps x 4 VGPRs: 288 at 128 -> 128), loaded
-// once.  The boards stream through a ring of kWsBuf LDS slots (64 pixel rows +
-// 16 zero rows each, the swizzle of conv_fwd_kernel) by direct global -> LDS
-// copies issued two boards ahead; per board a wave reads its B fragments (4
-// pixel tiles per k-step, ds_read_b128, the next k-step's issued before this
-// one's MFMAs) and runs CW / 16 x 4 x KS MFMAs, then stores 4 channels x 1
-// pixel per lane and tile (8 bytes).  One barrier per board.  The LDS address
-// of a B fragment is (atab[t][lane].i + slot) ^ (cb << 6): the table holds the
-// tap's shifted row (or its zero row) and the lane's chunk, and the 32-channel
-// block cb only flips chunk bits (row offsets are multiples of 128 bytes, slot
-// offsets of 2 KiB).
-// ---------------------------------------------------------------------------
-constexpr int kWsBuf = 3;
-#ifndef BB_CONV_WS_PF
-#define BB_CONV_WS_PF 2  // k-steps of B-fragment prefetch in conv_fwd_ws_kernel
-#endif
-constexpr int kWsPf = BB_CONV_WS_PF;
-#ifndef BB_CONV_WS_WAIT
-#define BB_CONV_WS_WAIT 0
-#endif
-constexpr int kWsZero = 16;
-
-int ws_grid(int nb) {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (!cus[dev]) {
-    int c = 0;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-    cus[dev] = c;
-  }
-  return nb < cus[dev] ? nb : cus[dev];
-}
-
-template <int CIN, int COUT>
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
-conv_fwd_ws_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int nb,
-                   const uint16_t* __restrict__ radd) {
-  constexpr int RB = CIN * 2;                       // bytes per pixel row
-  constexpr int NCH = CIN / 8;                      // 16-byte chunks per pixel row
-  constexpr int SLOT = (64 + kWsZero) * RB;         // one board + its zero rows
-  constexpr int NCB = CIN / 32;                     // 32-channel blocks per tap
-  constexpr int KS = 9 * NCB;                       // k-steps
-  constexpr int CW = COUT / 4;                      // output channels per wave
-  constexpr int NT = CW / 16;                       // 16-channel tiles per wave
-  constexpr int LPW = 64 * NCH / 256;               // direct copies per lane per board
-  static_assert(NT >= 1 && LPW >= 1, "shape");
-  __shared__ __attribute__((aligned(16))) uint8_t sm[kWsBuf * SLOT];
-  __shared__ int4 atab[9 * 64];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r16 = lane & 15, hq = lane >> 4;
-  const int G = gridDim.x;
-  const int co0 = wid * CW;
-
-  // copies of board b into slot s: LDS chunk e = 256 k + tid holds row e / NCH, logical chunk (e % NCH) ^ key
-  auto copy_board = [&](int b, int s) {
-    const uint16_t* src = x + (size_t)min(b, nb - 1) * 64 * CIN;
-#pragma unroll
-    for (int k = 0; k < LPW; ++k) {
-      const int e = k * 256 + tid, r = e / NCH, lc = (e % NCH) ^ fwd_key<CIN>(r);
-      glds16_async(src + r * CIN + lc * 8, sm + s * SLOT + (k * 256 + wid * 64) * 16);
-    }
-  };
-  const int b0 = blockIdx.x;
-  copy_board(b0, 0);
-  // weights -> registers: A fragment of tile j, k-step s: co = co0 + 16 j + r16, ci = 32 cb + 8 hq .. + 7 of tap t
-  // (issued in k-step order, so the first board's MFMAs start as the first fragments arrive)
-  bf16x8 wa[NT][KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-      wa[j][s] = *reinterpret_cast<const bf16x8*>(w + ((size_t)(s / NCB) * COUT + co0 + 16 * j + r16) * CIN +
-                                                  32 * (s % NCB) + 8 * hq);
-  copy_board(b0 + G, 1);
-  // zero rows of every slot (never overwritten: the copies fill rows 0..63 only)
-  for (int i = tid; i < kWsBuf * kWsZero * NCH; i += 256) {
-    const int s = i / (kWsZero * NCH), j = i % (kWsZero * NCH);
-    *reinterpret_cast<uint4*>(sm + s * SLOT + 64 * RB + j * 16) = make_uint4(0, 0, 0, 0);
-  }
-  // atab[t][lane].i: byte address in slot 0 of chunk (hq ^ key) of the row that pixel 16 i + r16 reads at tap t
-  // (the same for every wave; read one tap ahead, 4 VGPRs instead of 36 live addresses)
-  for (int e = tid; e < 9 * 64; e += 256) {
-    const int t = e / 64, l = e % 64, n = l & 15, q = l >> 4;
-    const int dy = t / 3 - 1, dx = t % 3 - 1;
-    int a[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = 16 * i + n, yy = (p >> 3) + dy, xc = (p & 7) + dx;
-      const int row = ((unsigned)yy < 8u && (unsigned)xc < 8u) ? yy * 8 + xc : 64 + ((p + 8 * dy + dx) & 15);
-      a[i] = row * RB + ((q ^ fwd_key<CIN>(row)) << 4);
-    }
-    atab[e] = make_int4(a[0], a[1], a[2], a[3]);
-  }
-  // board 0's copies have landed (the weight fragments and board 1's copies are younger and may be in flight:
-  // the compiler waits for each fragment before its first use)
-#if BB_CONV_WS_WAIT
-  BB_WAIT_VM_LGKM0(0);  // variant: every weight fragment (and board 1) has landed before the loop
-#else
-  BB_WAIT_VM_LGKM0(NT * KS + LPW);
-#endif
-  raw_barrier();
-
-  int slot = 0;
-  for (int b = b0; b < nb; b += G) {
-    // board b + 2 G into the slot board b - G used (every wave passed the barrier after reading it)
-    const int s2 = slot == 0 ? 2 : slot - 1;
-    copy_board(b + 2 * G, s2);
-    const int so = slot * SLOT;
-    uint2 ra[NT][4];
-    if (radd) {  // block-uniform
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          ra[j][i] = *reinterpret_cast<const uint2*>(radd + ((size_t)b * 64 + 16 * i + r16) * COUT + co0 + 16 * j +
-                                                     4 * hq);
-    }
-    f32x4 acc[NT][4];
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // B fragments read kWsPf k-steps ahead (one wave per SIMD: nothing else hides the LDS latency)
-    constexpr int PF = kWsPf;
-    int4 ad[3];
-    ad[0] = atab[lane];
-    ad[1] = atab[64 + lane];
-    bf16x8 bfr[PF + 1][4];
-    auto load = [&](int s) {
-      const int4 a = ad[(s / NCB) % 3];
-      const int x = (s % NCB) << 6;
-      bf16x8* d = bfr[s % (PF + 1)];
-      d[0] = *reinterpret_cast<const bf16x8*>(sm + ((a.x + so) ^ x));
-      d[1] = *reinterpret_cast<const bf16x8*>(sm + ((a.y + so) ^ x));
-      d[2] = *reinterpret_cast<const bf16x8*>(sm + ((a.z + so) ^ x));
-      d[3] = *reinterpret_cast<const bf16x8*>(sm + ((a.w + so) ^ x));
-    };
-#pragma unroll
-    for (int s = 0; s < PF; ++s) load(s);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (s % NCB == 0 && s / NCB + 2 < 9) ad[(s / NCB + 2) % 3] = atab[(s / NCB + 2) * 64 + lane];
-      if (s + PF < KS) load(s + PF);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][s], bfr[s % (PF + 1)][i], acc[j][i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // lane holds D[co0 + 16 j + 4 hq + reg][16 i + r16]
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        uint2 v;
-        v.x = pack2(acc[j][i][0], acc[j][i][1]);
-        v.y = pack2(acc[j][i][2], acc[j][i][3]);
-        if (radd) v = make_uint2(add2_bf16(v.x, ra[j][i].x), add2_bf16(v.y, ra[j][i].y));
-        *reinterpret_cast<uint2*>(y + ((size_t)b * 64 + 16 * i + r16) * COUT + co0 + 16 * j + 4 * hq) = v;
-      }
-    // next slot: its board's copies (issued one board earlier) must have landed for every wave.  Younger than
-    // them: this board's stores (NT * 4) and the copies of board b + 2 G (LPW) -- and, before those, the
-    // previous board's stores; waiting for at most LPW + 4 NT outstanding is therefore enough (and the radd
-    // loads, when present, already drained everything older)
-    BB_WAIT_VM(LPW + 4 * NT);
-    raw_barrier();
-    slot = slot == kWsBuf - 1 ? 0 : slot + 1;
-  }
-  BB_WAIT_VM(0);  // no copy into this workgroup's LDS may outlive it
-}
-
-// ---------------------------------------------------------------------------
 // weight gradient.  Workgroup (8 waves): one 64 (co) x 64 (ci) tile, all nine
 // taps, over a chunk of boards, 2 boards per LDS stage.  Stages go through a
 // ring of 4 LDS buffers by direct global -> LDS copies issued 3 stages ahead;
@@ -963,19 +779,9 @@ int wgrad_bpc(int nb, int nchunk) {
   return (bpc + kWgBoards - 1) / kWgBoards * kWgBoards;
 }
 
-#ifndef BB_CONV_FWD_WS
-#define BB_CONV_FWD_WS 0  // 1: forward / data gradient on conv_fwd_ws_kernel (parity-green, 46-48 vs 39.5 us per
-                          // 128 -> 128 call)
-#endif
-
 template <int CIN, int COUT>
 hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr) {
   if (nb <= 0) return hipErrorInvalidValue;
-  if (BB_CONV_FWD_WS) {
-    hipLaunchKernelGGL((conv_fwd_ws_kernel<CIN, COUT>), dim3(ws_grid(nb)), dim3(256), 0, s, (const uint16_t*)x,
-                       (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd);
-    return hipGetLastError();
-  }
   if (radd && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS)) return hipErrorInvalidValue;  // variant builds: no fused add
   hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>()), dim3(kFwdThreads), 0, s,
                      (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd);

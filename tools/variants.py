@@ -33,14 +33,8 @@ VARIANTS = {
     "asl4": ["-DBB_ASYNC_SLEEP=4"],
     # the one in-lane slot starts from the fewest-anchor piece (quick_least_bf)
     "aqp0": ["-DBB_ASYNC_QPICK=0"],
-    # forward / data-gradient convolutions on the weight-stationary kernel (conv_fwd_ws_kernel) instead of
-    # the streaming-weights one (conv_fwd_kernel)
-    "cws1": ["-DBB_CONV_FWD_WS=1"],
-    "cws1p1": ["-DBB_CONV_FWD_WS=1", "-DBB_CONV_WS_PF=1"],
-    "cws1p3": ["-DBB_CONV_FWD_WS=1", "-DBB_CONV_WS_PF=3"],
     # conv_fwd_kernel's stage loop rolled (address arithmetic per read) instead of unrolled
     "cfu0": ["-DBB_CONV_FWD_UNROLL=0"],
-    "cwsw": ["-DBB_CONV_FWD_WS=1", "-DBB_CONV_WS_WAIT=1"],
     # bb_step (step_fused_kernel): copy c's slot from the anchor-count rank c instead of hand slot c
     "sqp1": ["-DBB_STEP_QPICK=1"],
     "aphx": ["-DBB_ASYNC_PHILOX_EARLY=1"],
