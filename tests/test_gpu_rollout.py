@@ -108,9 +108,31 @@ def _assert_same(ref, got):
             assert np.array_equal(rs[k], gs[k]), f"state {k}"
 
 
-@pytest.mark.parametrize("n,steps", [(1000, 60), (4096, 90)])
+@pytest.mark.parametrize("n,steps", [(1, 40), (65, 30), (257, 40), (1000, 60), (4096, 90)])
 def test_rollout_equals_chained_steps(cuda, n, steps):
+    """Ragged and tiny batches too: one env (a workgroup with 255 dead lanes), 65 (a second env wave of one
+    env), 257 (a second workgroup of one env)."""
     _assert_same(_chained_steps(n, 0, steps, cuda), _rollout(n, 0, steps, cuda))
+
+
+def test_rollout_single_step_segments(cuda):
+    """Calls of T = 1 (bb_rollout then runs step_fused_kernel) between async calls continue one trajectory."""
+    _assert_same(_chained_steps(777, 5, 40, cuda), _rollout(777, 5, 40, cuda, splits=(1, 2, 9, 10)))
+
+
+def test_rollout_zero_steps_is_a_no_op(cuda):
+    env, a = _env(300, 0, cuda)
+    before = env.state()
+    rew = torch.full((1, 300), 7.0, device=cuda)
+    term = torch.full((1, 300), 9, dtype=torch.uint8, device=cuda)
+    nxt = torch.full((300,), -5, dtype=torch.int32, device=cuda)
+    env.rollout(0, a, rew, term, next_action=nxt, policy_seed=SEED)
+    torch.cuda.synchronize()
+    after = env.state()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k
+    assert bool((rew == 7.0).all()) and bool((term == 9).all()) and bool((nxt == -5).all())
+    env.close()
 
 
 def test_rollout_split_calls_and_offset(cuda):
