@@ -233,7 +233,21 @@ __device__ __forceinline__ bool channel_sums(const double* __restrict__ part, in
   const int lane = threadIdx.x & 63;
   if (c >= C) return false;
   a[0] = a[1] = a[2] = 0.0;
-  for (int blk = lane; blk < nb; blk += 64)
+  int blk = lane;
+  // 8 partial rows' loads in flight per lane before their (in-order) adds: the loop is a chain of
+  // dependent HBM latencies otherwise (one wave per channel, rows C * kQ doubles apart)
+  for (; blk + 7 * 64 < nb; blk += 8 * 64) {
+    double v[8][kQ];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int m = 0; m < kQ; ++m) v[j][m] = part[((int64_t)(blk + 64 * j) * C + c) * kQ + m];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int m = 0; m < kQ; ++m) a[m] += v[j][m];
+  }
+  for (; blk < nb; blk += 64)
     for (int m = 0; m < kQ; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
   for (int m = 0; m < kQ; ++m) a[m] = wave_sum(a[m]);
   return lane == 0;
