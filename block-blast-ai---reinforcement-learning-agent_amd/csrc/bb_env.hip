@@ -868,6 +868,9 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
 // 0: every drawn hand goes to the search waves
 #define BB_ASYNC_SLOTS 1
 #endif
+#ifndef BB_ASYNC_DIAG_DUPSEARCH
+#define BB_ASYNC_DIAG_DUPSEARCH 0  // diagnostics only: every search call run twice (tools/variants.py adup)
+#endif
 #ifndef BB_ASYNC_QPICK
 // 1: the one in-lane slot starts from the hand's fewest-anchor piece (quick_rank_bf), 1.308e10 vs 1.280e10
 // env-steps/s for slot 0 (0; profiles/r04/ab/q1_*)
@@ -989,8 +992,21 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
             lds_flag_store_release(&astat[rid], 2u);
           }
         };
+#if BB_ASYNC_DIAG_DUPSEARCH
+        const Pcg rng_dup = rng;
+#endif
         gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
                                                      a.pack_next, lds, dprof_p, 0, release);
+#if BB_ASYNC_DIAG_DUPSEARCH
+        {  // diagnostics only: the same search once more, results dropped (its instructions are the search
+           // waves' share of the kernel's SQ counts: counts of this build minus the shipped build's)
+          Pcg r2 = rng_dup;
+          uint32_t ids2 = 0;
+          gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, r2, ids2, t.row, t.d, jt, lane, a.pack_first,
+                                                       a.pack_next, lds);
+          if (ids2 == 0x7FFFFFFFu && r2.hi == 1ull) lds[lane] = ids2;  // keeps the call
+        }
+#endif
 #if BB_ASYNC_DIAG
         dcyc += __builtin_amdgcn_s_memtime() - c0;
         dcalls += 1;

@@ -33,6 +33,9 @@ VARIANTS = {
     "asl4": ["-DBB_ASYNC_SLEEP=4"],
     # the one in-lane slot starts from the fewest-anchor piece (quick_least_bf)
     "aqp0": ["-DBB_ASYNC_QPICK=0"],
+    # diagnostics: every search call run a second time, results dropped (search waves' share of the SQ counts)
+    "adup": ["-DBB_ASYNC_DIAG_DUPSEARCH=1"],
+    "adupdiag": ["-DBB_ASYNC_DIAG_DUPSEARCH=1", "-DBB_ASYNC_DIAG=1"],
     # conv_fwd_kernel's stage loop rolled (address arithmetic per read) instead of unrolled
     "cfu0": ["-DBB_CONV_FWD_UNROLL=0"],
     # bb_step (step_fused_kernel): copy c's slot from the anchor-count rank c instead of hand slot c
