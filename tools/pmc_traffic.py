@@ -9,8 +9,8 @@ FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md
 (§HBM): on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads,
 so it is doubled; WRITE_SIZE is taken as is.  The per-launch figure is the
 mean over dispatches of each bb_step kernel, summed over the two kernels of
-one bb_step (step_kernel + escalate_kernel), or the one rollout_kernel of a
-bb_rollout launch (--kernels rollout_kernel --steps-per-launch T).
+one bb_step (step_fused_kernel, or step_kernel + escalate_kernel), or the rollout_async_kernel of a
+bb_rollout launch (--kernels rollout_async_kernel --steps-per-launch T).
 """
 import argparse
 import csv
