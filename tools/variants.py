@@ -63,6 +63,7 @@ VARIANTS = {
     # NOT a correct convolution: cdiag1 = no output stores, cdiag2 = one tap of nine
     "cf64r3": ["-DBB_CONV_FWD_SCI=64", "-DBB_CONV_FWD_RING=3"],
     "cf32r3": ["-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=3"],
+    "cf32r4": ["-DBB_CONV_FWD_SCI=32", "-DBB_CONV_FWD_RING=4"],
     "cfb1": ["-DBB_CONV_FWD_BOARDS=1"],
     "cm32": ["-DBB_CONV_MFMA16=0"],
     "cw16": ["-DBB_CONV_WG16=1"],
