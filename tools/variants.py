@@ -78,6 +78,8 @@ VARIANTS = {
     "sdef": ["-mllvm", "-amdgpu-sched-strategy=default"],
     "smem": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
     "o2": ["-O2"],
+    "ut300": ["-mllvm", "-unroll-threshold=300"],
+    "ut1200": ["-mllvm", "-unroll-threshold=1200"],
 }
 
 
@@ -86,9 +88,10 @@ def build(name: str) -> str:
     os.makedirs(OUT, exist_ok=True)
     out = os.path.join(OUT, f"libbbvec_{name}.so")
     base = [f for f in HIPCC_FLAGS if not f.startswith("--offload-arch")]  # the shipped flags (runtime/build.py)
-    if any(f.startswith("-amdgpu-sched-strategy") for f in flags):  # a scheduler variant replaces the shipped one
-        i = base.index("-mllvm")
-        del base[i:i + 2]
+    for opt in ("-amdgpu-sched-strategy", "-unroll-threshold"):  # a variant of a shipped -mllvm option replaces it
+        if any(f.startswith(opt) for f in flags):
+            i = next(k for k in range(len(base)) if base[k].startswith(opt))
+            del base[i - 1:i + 1]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *base, *flags, f"-I{os.path.join(REPO, 'include')}",
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
     subprocess.run(cmd, check=True)
