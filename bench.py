@@ -45,6 +45,42 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 POLICY_SEED = 0xB10C
 
 
+def host_facts() -> dict:
+    """the host the CPU baselines ran on -- CPU model, visible cores, torch threads."""
+    import torch
+
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "torch_threads": torch.get_num_threads(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def load_valu(n_envs: int, steps_per_launch: int):
+    """The rollout kernel's instruction-issue record (its binding resource) from a committed
+    rocprofv3 SQ-counter run (profiles/sq_rollout_kernel.json, tools/sq_summary.py --json), or None when it
+    was taken on another shape."""
+    p = os.path.join(REPO, "profiles", "sq_rollout_kernel.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if int(d.get("n_envs", -1)) != n_envs or int(d.get("steps_per_launch", -1)) != steps_per_launch:
+        return None
+    keys = ("valu_insts_per_launch", "valu_insts_per_env_step", "wave_cycles_per_env_step",
+            "cycles_per_valu_per_simd", "issue_floor_cycles", "issue_frac", "profiled_ms", "build_id")
+    out = {k: d[k] for k in keys if k in d}
+    out["source"] = "profiles/sq_rollout_kernel.json (rocprofv3 --pmc SQ_INSTS_VALU, SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE)"
+    return out
+
+
 def cpu_baseline(seconds: float = 12.0) -> dict:
     """Reference path on the host: 64 envs stepped sequentially by the CPU
     port of src/environment/wrappers.py (cell loops like the reference), with
@@ -74,6 +110,8 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
         "kind": "port",
         "sample": f"{n} envs x {steps} vec steps ({n * steps} env-steps, {el:.1f}s), random legal actions, "
                   "CPU port of wrappers.py/block_blast_env.py/engine.py (oracle/bb_game.py), 1 Python thread",
+        "reference_loop": "/root/reference/src/environment/wrappers.py:75-116 (sequential BlockBlastEnv.step loop)",
+        **host_facts(),
     }
 
 
@@ -85,6 +123,7 @@ def cpu_baseline_native(seconds: float = 8.0, n: int = 65536, T: int = 16) -> di
     number.  Bounded to ~`seconds`."""
     import torch
 
+    from runtime import lib as L
     from runtime.device_env import DeviceEnvBatch
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
@@ -114,6 +153,9 @@ def cpu_baseline_native(seconds: float = 8.0, n: int = 65536, T: int = 16) -> di
         "sample": f"{n} envs x {T * launches} env-steps ({launches} bb_rollout calls of T={T}, {el:.1f}s), fused "
                   f"random legal-action policy, host backend libbbvec_host.so (C++ bitboards, OpenMP, "
                   f"{threads} threads)",
+        "reference_loop": "/root/reference/src/environment/wrappers.py:75-116, restated natively over all envs",
+        "build_id": L.build_id(host=True),
+        **host_facts(),
     }
 
 
@@ -173,6 +215,7 @@ def main() -> None:
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    from runtime import lib as L
     from runtime.device_env import DeviceEnvBatch
 
     n = args.envs
@@ -303,7 +346,11 @@ def main() -> None:
                 "kernel_avg_ms": round(kern_ms, 5),
                 "algo_bytes_per_launch": algo_bytes,
             },
+            "build_id": L.build_id(),
         }
+        if args.mode == "rollout":
+            # the binding resource is instruction issue, not bytes: the committed SQ counters
+            out["roofline"]["valu"] = load_valu(n, T)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"] = cb

@@ -142,9 +142,18 @@ StepArgs base_args(const bb_env* env) {
 
 }  // namespace
 
+// The build id (runtime/build.py: a hash of the sources, include/bbvec.h and the hipcc flags, passed as
+// -DBB_BUILD_ID).  The marker prefix lets build.py read the id out of the .so without loading it.
+#ifndef BB_BUILD_ID
+#define BB_BUILD_ID "unhashed"
+#endif
+static const char kBuildIdMarker[] = "bbvec-build-id:" BB_BUILD_ID;
+
 extern "C" {
 
 int bb_abi_version(void) { return BB_ABI_VERSION; }
+
+const char* bb_build_id(void) { return kBuildIdMarker + 15; }
 
 const char* bb_last_error(const bb_env* env) { return env ? env->err.c_str() : g_create_err.c_str(); }
 
@@ -308,10 +317,19 @@ int bb_reset(bb_env* env, const uint8_t* d_env_mask, void* stream) {
   if (d_env_mask && status_fail(env, "bb_reset (masked)") != BB_OK) return BB_ERR_DEVICE;
   DeviceGuard g(env->device);
   hipError_t st = hipSuccess;
-  if (!d_env_mask && (env->broken || __atomic_load_n(env->h_status, __ATOMIC_ACQUIRE))) {
-    // a failed launch may still be running: let it finish before its status word is cleared
-    st = hipStreamSynchronize((hipStream_t)stream);
-    __atomic_store_n(env->h_status, 0u, __ATOMIC_RELEASE);
+  if (!d_env_mask) {
+    // A full reset clears the status word in stream order: a rollout that is still queued or running ahead
+    // of this reset may yet raise it, so the word is cleared only after that launch has finished -- by a
+    // stream synchronisation and a host store, or (under graph capture, where a host sync is illegal) by a
+    // device write queued on the stream.
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    if (cs == hipStreamCaptureStatusNone) {
+      st = hipStreamSynchronize((hipStream_t)stream);
+      if (st == hipSuccess) __atomic_store_n(env->h_status, 0u, __ATOMIC_RELEASE);
+    } else {
+      st = hipMemsetAsync(env->d.status, 0, sizeof(uint32_t), (hipStream_t)stream);
+    }
   }
   if (st == hipSuccess) st = launch_reset(env->d, env->d_rows, env->d_dtab, d_env_mask, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(env, st, "bb_reset");
@@ -406,6 +424,8 @@ int bb_sync(bb_env* env, void* stream) {
 
 int bb_obs(bb_env* env, float* d_x, int8_t* d_mask_i8, float* d_mask_f32, uint64_t* d_mask_bits, void* stream) {
   if (!env) return BB_ERR_ARG;
+  if (status_fail(env, "bb_obs") != BB_OK) return BB_ERR_DEVICE;  // the state an incomplete launch left
+  if (env->broken) return broken_fail(env, "bb_obs");
   DeviceGuard g(env->device);
   hipStream_t s = (hipStream_t)stream;
   hipError_t st = launch_expand(env->d.board, env->d.hand, env->d.mask, nullptr, env->d_rows, env->n, d_x,
@@ -426,6 +446,8 @@ int bb_device_ptrs(bb_env* env, uint64_t** d_board, uint32_t** d_hand, uint64_t*
 
 int bb_snapshot(bb_env* env, uint64_t* d_board, uint32_t* d_hand, uint64_t* d_mask_bits, void* stream) {
   if (!env) return BB_ERR_ARG;
+  if (status_fail(env, "bb_snapshot") != BB_OK) return BB_ERR_DEVICE;
+  if (env->broken) return broken_fail(env, "bb_snapshot");
   DeviceGuard g(env->device);
   hipStream_t s = (hipStream_t)stream;
   const size_t n = (size_t)env->n;

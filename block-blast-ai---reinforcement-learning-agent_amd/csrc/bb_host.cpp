@@ -347,9 +347,16 @@ Out step_env(bb_env* e, int i, int act, bb_info* info, int64_t* final_score, int
 
 }  // namespace
 
+#ifndef BB_BUILD_ID
+#define BB_BUILD_ID "unhashed"
+#endif
+static const char kBuildIdMarker[] = "bbvec-build-id:" BB_BUILD_ID;  // runtime/build.py host_source_id
+
 extern "C" {
 
 int bb_abi_version(void) { return BB_ABI_VERSION; }
+
+const char* bb_build_id(void) { return kBuildIdMarker + 15; }
 
 const char* bb_last_error(const bb_env* env) { return env ? env->err.c_str() : g_create_err.c_str(); }
 

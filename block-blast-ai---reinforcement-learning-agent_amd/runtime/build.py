@@ -1,6 +1,7 @@
 """Build libbbvec.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -36,20 +37,50 @@ def _hipcc() -> str:
     return "hipcc"
 
 
-def _stale(out: str, inputs) -> bool:
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(p) > t for p in inputs)
+MARKER = b"bbvec-build-id:"  # csrc/bb_capi.cpp / bb_host.cpp kBuildIdMarker
+HEADER = os.path.join(REPO_DIR, "include", "bbvec.h")
+
+
+def _source_id(files, flags) -> str:
+    """First 16 hex digits of SHA-256 over the flags and every input file's name and bytes: the id a
+    library built from exactly these sources carries (bb_build_id)."""
+    h = hashlib.sha256()
+    h.update("\0".join(flags).encode())
+    for f in files:
+        h.update(b"\0" + os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def source_id() -> str:
+    """The build id of libbbvec.so for the sources in this tree."""
+    return _source_id([os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [HEADER], HIPCC_FLAGS)
+
+
+def host_source_id() -> str:
+    """The build id of libbbvec_host.so for the sources in this tree."""
+    return _source_id([os.path.join(CSRC, s) for s in HOST_SOURCES + HOST_HEADERS] + [HEADER], HOST_FLAGS)
+
+
+def built_id(path: str):
+    """The build id embedded in a built library (read from its bytes; the library is not loaded), or None."""
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    k = data.find(MARKER)
+    return data[k + len(MARKER):k + len(MARKER) + 16].decode("ascii", "replace") if k >= 0 else None
 
 
 def build_lib(force: bool = False, verbose: bool = True) -> str:
-    inputs = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(REPO_DIR, "include", "bbvec.h"),
-                                                                  os.path.abspath(__file__)]  # flags live here
-    if not force and not _stale(LIB_PATH, inputs):
+    """Build libbbvec.so unless the one in the tree already carries the id of these sources."""
+    sid = source_id()
+    if not force and built_id(LIB_PATH) == sid:
         return LIB_PATH
     tmp = LIB_PATH + ".tmp"
-    cmd = [_hipcc(), *HIPCC_FLAGS, f"-I{os.path.join(REPO_DIR, 'include')}",
+    cmd = [_hipcc(), *HIPCC_FLAGS, f'-DBB_BUILD_ID="{sid}"', f"-I{os.path.join(REPO_DIR, 'include')}",
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
@@ -65,12 +96,11 @@ HOST_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-fo
 
 
 def build_host_lib(force: bool = False, verbose: bool = True) -> str:
-    inputs = [os.path.join(CSRC, s) for s in HOST_SOURCES + HOST_HEADERS] + [
-        os.path.join(REPO_DIR, "include", "bbvec.h"), os.path.abspath(__file__)]
-    if not force and not _stale(HOST_LIB_PATH, inputs):
+    sid = host_source_id()
+    if not force and built_id(HOST_LIB_PATH) == sid:
         return HOST_LIB_PATH
     tmp = HOST_LIB_PATH + ".tmp"
-    cmd = [os.environ.get("CXX", "g++"), *HOST_FLAGS, f"-I{os.path.join(REPO_DIR, 'include')}",
+    cmd = [os.environ.get("CXX", "g++"), *HOST_FLAGS, f'-DBB_BUILD_ID="{sid}"', f"-I{os.path.join(REPO_DIR, 'include')}",
            *[os.path.join(CSRC, s) for s in HOST_SOURCES], "-o", tmp]
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)

@@ -60,7 +60,7 @@ class Info(C.Structure):
     ]
 
 
-ABI_VERSION = 5  # include/bbvec.h BB_ABI_VERSION
+ABI_VERSION = 6  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -119,6 +119,7 @@ _F = C.c_float
 # name -> (restype, argtypes); exactly the entry points of include/bbvec.h
 SIGNATURES = {
     "bb_abi_version": (C.c_int, []),
+    "bb_build_id": (C.c_char_p, []),
     "bb_create": (C.c_int, [_I32, _I32, C.POINTER(RewardCfg), _I32, C.POINTER(_P)]),
     "bb_destroy": (None, [_P]),
     "bb_last_error": (C.c_char_p, [_P]),
@@ -163,7 +164,7 @@ SIGNATURES = {
 }
 
 # the env entry points, which the host backend (libbbvec_host.so) exports too
-HOST_SYMBOLS = ("bb_abi_version", "bb_create", "bb_destroy", "bb_last_error", "bb_num_envs", "bb_pcg64_seed",
+HOST_SYMBOLS = ("bb_abi_version", "bb_build_id", "bb_create", "bb_destroy", "bb_last_error", "bb_num_envs", "bb_pcg64_seed",
                 "bb_seed", "bb_reset", "bb_step", "bb_rollout", "bb_sync", "bb_obs", "bb_device_ptrs", "bb_snapshot",
                 "bb_get_state", "bb_set_state", "bb_random_actions")
 
@@ -192,9 +193,30 @@ def load(path: str | None = None):
         v = lib.bb_abi_version()
         if v != ABI_VERSION:
             raise BBNativeError(f"libbbvec ABI version mismatch ({v}, expected {ABI_VERSION})")
+        if path is None and "BBVEC_LIB" not in os.environ:
+            _check_build_id(lib, p, host=False)
         if path is None:
             _lib = lib
         return lib
+
+
+def _check_build_id(lib, p: str, host: bool) -> None:
+    """Refuse a library that was not built from the sources beside it (bb_build_id against
+    runtime/build.py's hash of csrc/, include/bbvec.h and the flags).  Explicit variant builds
+    (load(path), BBVEC_LIB) are diagnostics and skip the check."""
+    from . import build as B
+
+    want = B.host_source_id() if host else B.source_id()
+    have = lib.bb_build_id().decode()
+    if have != want:
+        raise BBNativeError(
+            f"{os.path.basename(p)} was built from other sources (build id {have}, these sources {want}); "
+            "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
+
+
+def build_id(host: bool = False) -> str:
+    """The loaded library's build id (bb_build_id)."""
+    return (load_host() if host else load()).bb_build_id().decode()
 
 
 def load_host():
@@ -214,6 +236,7 @@ def load_host():
             fn.argtypes = args
         if lib.bb_abi_version() != ABI_VERSION:
             raise BBNativeError("libbbvec_host ABI version mismatch")
+        _check_build_id(lib, HOST_LIB_PATH, host=True)
         _host = lib
         return lib
 

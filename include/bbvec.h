@@ -32,9 +32,10 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 5  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
+#define BB_ABI_VERSION 6  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
                               4: bb_conv_in_* and bb_relu_bias_grad* removed;
-                              5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed */
+                              5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed;
+                              6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -126,6 +127,10 @@ typedef struct bb_state_view {
  * vec-env semantics (wrappers.py:97-102), 0 the single-env semantics.  The new
  * envs are unseeded until bb_seed + bb_reset. */
 int bb_abi_version(void);
+/* The id of the sources this library was built from: the first 16 hex digits of a SHA-256 over csrc/,
+ * include/bbvec.h and the compiler flags (runtime/build.py source_id).  runtime/lib.load() refuses a
+ * library whose id is not that of the sources beside it.  No reference counterpart. */
+const char* bb_build_id(void);
 int bb_create(int32_t num_envs, int32_t device, const bb_reward_cfg* cfg,
               int32_t autoreset, bb_env** out);
 void bb_destroy(bb_env* env);

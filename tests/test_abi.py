@@ -24,7 +24,29 @@ def test_header_and_binding_agree():
 def test_library_exports_every_symbol(lib):
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.bb_abi_version() == L.ABI_VERSION == 5
+    assert lib.bb_abi_version() == L.ABI_VERSION == 6
+
+
+def test_build_id_is_these_sources(lib):
+    """bb_build_id ties the binary to HEAD's sources: the id is the hash of csrc/, include/bbvec.h and the
+    flags, the .so carries it where build.py reads it without loading, and load() refuses a mismatch."""
+    from runtime import build as B
+
+    sid = B.source_id()
+    assert len(sid) == 16 and lib.bb_build_id().decode() == sid == B.built_id(L.LIB_PATH)
+    assert L.build_id() == sid
+    host = B.build_host_lib(verbose=False)
+    assert B.built_id(host) == B.host_source_id() == L.build_id(host=True)
+
+
+def test_stale_library_is_refused(lib, tmp_path, monkeypatch):
+    """A library whose id differs from the sources beside it is refused by name, not loaded silently."""
+    from runtime import build as B
+
+    monkeypatch.setattr(B, "source_id", lambda: "0" * 16)
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(L.BBNativeError, match="built from other sources"):
+        L.load()
 
 
 def test_struct_sizes(lib):

@@ -140,8 +140,19 @@ def test_async_iteration_cap_fails_loudly(cuda, monkeypatch):
         dev.rollout(steps, a0, *bufs, policy_seed=SEED)
     with pytest.raises(L.BBNativeError, match=r"\(-4\)"):
         dev.state()
+    with pytest.raises(L.BBNativeError, match=r"bb_obs failed \(-4\)"):
+        dev.obs(mask_bits=mb)
+    with pytest.raises(L.BBNativeError, match=r"bb_snapshot failed \(-4\)"):
+        dev.snapshot(torch.zeros(n, dtype=torch.int64, device=cuda), None, None)
     dev.reset()  # a full reset clears the status word
     dev.sync()
+    dev.state()
+    # a capped launch still queued when the full reset is issued: the reset clears the word in stream
+    # order, after that launch has raised it, so the fresh handle's next calls succeed
+    dev.rollout(steps, a0, *bufs, policy_seed=SEED)
+    dev.reset()
+    dev.sync()
+    dev.obs(mask_bits=mb)
     dev.state()
     ok.rollout(steps, a0, *bufs, policy_seed=SEED)
     ok.sync()
