@@ -819,6 +819,31 @@ extern "C" int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, in
   return BB_OK;
 }
 
+extern "C" int bb_conv3x3_f32_prep(const float* d_w, int32_t cin, int32_t cout, int32_t w_layout, float* d_wf,
+                                   float* d_wd, void* stream) {
+  if (!conv3x3_f32_supported(cin, cout))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_prep: (cin, cout) must be (128, 128), (64, 128) or (128, 64)");
+  if (w_layout != 0 && w_layout != 1) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_prep: w_layout must be 0 or 1");
+  if (!d_w || (!d_wf && !d_wd)) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_prep: NULL argument");
+  if (!al16(d_wf) || !al16(d_wd)) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_prep: outputs must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_f32_prep(d_w, cin, cout, w_layout, d_wf, d_wd, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_f32_prep");
+  return BB_OK;
+}
+
+extern "C" int bb_conv3x3_f32_forward(const float* d_x, const float* d_w, int32_t N, int32_t cin, int32_t cout,
+                                      float* d_y, void* stream) {
+  if (N <= 0) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_forward: empty batch");
+  if (!conv3x3_f32_supported(cin, cout))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_forward: (cin, cout) must be (128, 128), (64, 128) or (128, 64)");
+  if (!d_x || !d_w || !d_y) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_forward: NULL argument");
+  if (!al16(d_x) || !al16(d_w) || !al16(d_y))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_f32_forward: tensors must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_f32_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_f32_forward");
+  return BB_OK;
+}
+
 static_assert(BB_OPT_MAX_TENSORS == kOptMaxTensors, "bbvec.h / bb_env_internal.h tensor-table size");
 
 extern "C" int64_t bb_adam_clip_workspace_bytes(int32_t num_tensors, const int64_t* h_numel) {

@@ -1,0 +1,227 @@
+// bb_conv32.hip -- the CNN's 3x3 / pad-1 convolutions on 8x8 boards in fp32 (gfx950), accumulated so that
+// the result is as close to the exact sum as one fp32 rounding allows.
+//
+// The policy's fp32 forward (network.py:75-117, ResidualBlock network.py:14-30) runs in training mode in the
+// rollout (scripts/train.py:122 keeps agent.train(): batch-statistics BatchNorm after every convolution).
+// MIOpen's fp32 128-channel convolutions (K = 9 x 128 = 1,152 products per output) accumulate in one long
+// order, and the batch-statistics BatchNorms amplify that rounding: the logits ended 1.28e-5 from the fp64
+// truth, over north_star's 1e-5.  Here every output is a sum of short fp32 chains: each
+// 16-channel block of one tap is one v_mfma_f32_16x16x4_f32 chain of 16 products (exact fp32, bit-for-bit an
+// fmaf chain, MI355X_MICROARCH.md), and the blocks are added in fp64 (72 blocks at 128 channels), rounded to
+// fp32 once at the end.  The error is then ~0.5 ulp of the result plus a 16-term chain's, against a
+// 1,152-term chain's.
+//
+//   y[b,p,co] = sum_{t,ci} x[b,p+d_t,ci] * w[co,ci,t],   d_t = (t/3 - 1, t%3 - 1), zero outside the board
+//   dx[b,q,ci] = the same kernel over dy with w'[t'][ci][co] = w[co][ci][8 - t']
+//
+// Layouts: x, y, dy, dx f32 NHWC (channels_last), [nb][64][C]; weight images f32 [9][COUT][CIN] (forward) and
+// [9][CIN][COUT] tap-reversed (data gradient), written by conv32_prep_kernel from nn.Conv2d's [COUT][CIN][3][3]
+// (w_layout 0) or a channels_last parameter [COUT][3][3][CIN] (w_layout 1).
+//
+// Workgroup: 8 waves, 2 boards (128 pixel rows) x all COUT.  Waves: COUT 128 -> 2 (co) x 4 (px) waves of 64 co x
+// 32 px; COUT 64 -> 1 x 8 waves of 64 co x 16 px.  The input tile (2 boards, plus 16 zero rows for the taps
+// that leave the board) is copied to LDS once (global -> LDS direct); the weights stream through a 2-slot LDS
+// ring in stages of one tap x 32 input channels.  MFMA operands: lane l of a 16x16x4 step holds
+// A[co0 + (l & 15)][k] and B[k][px0 + (l & 15)] for k = 4 (l >> 4) + s of a 16-channel block, s = 0..3 the
+// step: one ds_read_b128 per operand and block (the k order inside a block is a permutation of the channels,
+// the same for A and B).  LDS rows are XOR-swizzled by 16-byte chunk (input: chunk ^ (row & 15); weights:
+// chunk ^ ((co >> 1) & 7)) so the 16 lanes of each ds_read_b128 group hit 16 different bank quads; a zero row
+// keeps the key of the row it replaces.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bb_env_internal.h"
+
+namespace bb {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kC32Threads = 512;
+constexpr int kC32Boards = 2;
+constexpr int kC32Rows = kC32Boards * 64;
+constexpr int kC32Zero = 16;
+constexpr int kC32Sci = 32;  // input channels per weight stage
+constexpr int kC32Ring = 2;
+#ifndef BB_CONV32_BLOCK
+#define BB_CONV32_BLOCK 16  // channels per fp32 MFMA chain before the fp64 add (16 or 32)
+#endif
+
+__device__ __forceinline__ void c32_glds16(const void* g, uint8_t* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+__global__ void __launch_bounds__(256) conv32_prep_kernel(const float* __restrict__ w, int cout, int cin, int wl,
+                                                          float* __restrict__ wf, float* __restrict__ wd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= cout * cin * 9) return;
+  const int co = i / (9 * cin);
+  const int t = wl ? (i / cin) % 9 : i % 9;
+  const int ci = wl ? i % cin : (i / 9) % cin;
+  const float v = w[i];
+  if (wf) wf[(t * cout + co) * cin + ci] = v;
+  if (wd) wd[((8 - t) * cin + ci) * cout + co] = v;
+}
+
+template <int CIN, int COUT>
+__global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ w, float* __restrict__ y,
+                                                                 int nb) {
+  constexpr int RB = CIN * 4;                       // bytes per pixel row
+  constexpr int NCH = CIN / 4;                      // 16-byte chunks per pixel row (16 or 32)
+  constexpr int XBYTES = (kC32Rows + kC32Zero) * RB;
+  constexpr int NCB = CIN / kC32Sci;                // weight stages per tap
+  constexpr int NS = 9 * NCB;                       // stages
+  constexpr int WROW = kC32Sci * 4;                 // 128-byte weight rows (8 chunks)
+  constexpr int WBYTES = COUT * WROW;
+  constexpr int NW = kC32Threads / 64;
+  constexpr int GPW = WBYTES / 1024 / NW;           // 1-KB weight copies per wave per stage
+  constexpr int WN = COUT / 64;                     // waves along co
+  constexpr int WM = NW / WN;                       // waves along px
+  constexpr int TN = 4;                             // 16-co tiles per wave
+  constexpr int TM = kC32Rows / WM / 16;            // 16-px tiles per wave
+  constexpr int KB = kC32Sci / 16;                  // 16-channel blocks per stage
+  constexpr int FL = BB_CONV32_BLOCK / 16;          // blocks per fp64 add
+  static_assert(NCH >= 16 && GPW >= 1 && TM >= 1, "shape");
+  __shared__ __attribute__((aligned(16))) uint8_t sm[XBYTES + kC32Ring * WBYTES];
+  uint8_t* const xs = sm;
+
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int b0 = blockIdx.x * kC32Boards;
+  const int r16 = lane & 15, g = lane >> 4;
+
+  // input tile: physical chunk e = 64 k + lane holds row e / NCH, logical chunk (e % NCH) ^ (row & 15)
+  for (int k = wid; k < kC32Rows * NCH / 64; k += NW) {
+    const int e = k * 64 + lane, r = e / NCH, lc = (e % NCH) ^ (r & 15);
+    const int b = min(b0 + (r >> 6), nb - 1);  // boards past the batch read the last one (never stored)
+    c32_glds16(x + (size_t(b) * 64 + (r & 63)) * CIN + lc * 4, xs + k * 1024);
+  }
+  auto stage_w = [&](int st) {  // stage st: tap st / NCB, channels 32 (st % NCB) ... -> slot st % 2
+    uint8_t* wb = sm + XBYTES + (st % kC32Ring) * WBYTES;
+    const float* ws = w + (size_t)(st / NCB) * COUT * CIN + (st % NCB) * kC32Sci;
+#pragma unroll
+    for (int kq = 0; kq < GPW; ++kq) {
+      const int k = wid + kq * NW;
+      const int e = k * 64 + lane, r = e / 8, lc = (e % 8) ^ ((r >> 1) & 7);
+      c32_glds16(ws + r * CIN + lc * 4, wb + k * 1024);
+    }
+  };
+  stage_w(0);
+  for (int i = tid; i < kC32Zero * NCH; i += kC32Threads)
+    *reinterpret_cast<uint4*>(xs + kC32Rows * RB + i * 16) = make_uint4(0, 0, 0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  const int co0 = (wid % WN) * 64;
+  const int px0 = (wid / WN) * (kC32Rows / WM);
+  int abase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int co = co0 + 16 * j + r16;
+    abase[j] = co * WROW;
+  }
+  double dacc[TN][TM][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dacc[j][i][e] = 0.0;
+  int brow[TM];
+
+  for (int st = 0; st < NS; ++st) {
+    if (st + 1 < NS) stage_w(st + 1);  // its slot was last read in stage st - 1, before that stage's barrier
+    const int cb = st % NCB;
+    if (cb == 0) {
+      const int t = st / NCB, dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int px = px0 + 16 * i + r16;
+        const int p = px & 63, yy = (p >> 3) + dy, xc = (p & 7) + dx;
+        brow[i] = ((unsigned)yy < 8u && (unsigned)xc < 8u) ? (px & ~63) + yy * 8 + xc
+                                                           : kC32Rows + ((px + 8 * dy + dx) & 15);
+      }
+    }
+    const uint8_t* wb = sm + XBYTES + (st % kC32Ring) * WBYTES;
+    f32x4 af[KB][TN], bf[KB][TM];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = co0 + 16 * j + r16;
+        af[kb][j] = *reinterpret_cast<const f32x4*>(wb + abase[j] + (((4 * kb + g) ^ ((co >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = brow[i];
+        bf[kb][i] = *reinterpret_cast<const f32x4*>(xs + row * RB + (((cb * 8 + 4 * kb + g) ^ (row & 15)) << 4));
+      }
+    }
+#pragma unroll
+    for (int kb0 = 0; kb0 < KB; kb0 += FL) {
+      f32x4 acc[TN][TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = kb0; kb < kb0 + FL; ++kb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[kb][j][s], bf[kb][i][s], acc[j][i], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dacc[j][i][e] += (double)acc[j][i][e];
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the next stage's weights (this wave's copies; the barrier covers the rest)
+    __syncthreads();
+  }
+  // D[co0 + 16 j + 4 g + e][px0 + 16 i + r16]: 4 consecutive channels of one pixel = one 16-byte store
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int px = px0 + 16 * i + r16;
+    if (b0 + (px >> 6) >= nb) continue;
+    float* yo = y + (size_t(b0) * 64 + px) * COUT + co0 + 4 * g;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      *reinterpret_cast<f32x4*>(yo + 16 * j) = f32x4{(float)dacc[j][i][0], (float)dacc[j][i][1],
+                                                     (float)dacc[j][i][2], (float)dacc[j][i][3]};
+  }
+}
+
+template <int CIN, int COUT>
+hipError_t c32_fwd_t(const float* x, const float* w, int nb, float* y, hipStream_t s) {
+  hipLaunchKernelGGL((conv32_fwd_kernel<CIN, COUT>), dim3((nb + kC32Boards - 1) / kC32Boards), dim3(kC32Threads), 0,
+                     s, x, w, y, nb);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool conv3x3_f32_supported(int cin, int cout) {
+  return (cin == 128 && cout == 128) || (cin == 64 && cout == 128) || (cin == 128 && cout == 64);
+}
+
+hipError_t launch_conv3x3_f32_prep(const float* w, int cin, int cout, int wl, float* wf, float* wd, hipStream_t s) {
+  const int n = cout * cin * 9;
+  hipLaunchKernelGGL(conv32_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, cout, cin, wl, wf, wd);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv3x3_f32_forward(const float* x, const float* w, int nb, int cin, int cout, float* y,
+                                      hipStream_t s) {
+  if (nb <= 0 || !conv3x3_f32_supported(cin, cout)) return hipErrorInvalidValue;
+  if (cin == 64) return c32_fwd_t<64, 128>(x, w, nb, y, s);
+  if (cout == 64) return c32_fwd_t<128, 64>(x, w, nb, y, s);
+  return c32_fwd_t<128, 128>(x, w, nb, y, s);
+}
+
+}  // namespace bb

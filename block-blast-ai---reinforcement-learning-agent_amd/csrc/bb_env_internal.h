@@ -121,6 +121,11 @@ hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin,
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);
 
+bool conv3x3_f32_supported(int cin, int cout);
+hipError_t launch_conv3x3_f32_prep(const float* w, int cin, int cout, int wl, float* wf, float* wd, hipStream_t s);
+hipError_t launch_conv3x3_f32_forward(const float* x, const float* w, int nb, int cin, int cout, float* y,
+                                      hipStream_t s);
+
 int64_t ppo_loss_workspace_bytes(int B);
 hipError_t launch_ppo_loss_forward(const float* logits, const float* values, const float* mask, const int64_t* actions,
                                    const float* old_logp, const float* adv, const float* ret, int B, float clip,

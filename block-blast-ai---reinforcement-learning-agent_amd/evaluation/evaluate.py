@@ -32,16 +32,19 @@ def _summary(scores, lengths, lines, combos) -> Dict[str, Any]:
     }
 
 
-def _evaluate_sequential(agent, num_episodes: int, deterministic: bool, render: bool, seed: int):
+def _evaluate_sequential(agent, num_episodes: int, deterministic: bool, render: bool, seed: int,
+                         record_actions: bool = False):
     from environment.block_blast_env import BlockBlastEnv
 
     env = BlockBlastEnv(render_mode="human" if render else None, seed=seed)
-    scores, lengths, lines, combos = [], [], [], []
+    scores, lengths, lines, combos, actions = [], [], [], [], []
     for ep in range(num_episodes):
         obs, info = env.reset(seed=seed + ep)
         done, n, score = False, 0, 0
+        actions.append([])
         while not done:
             action, _ = agent.select_action(obs, deterministic=deterministic)
+            actions[-1].append(int(action))
             obs, _, terminated, truncated, info = env.step(action)
             done = terminated or truncated
             n += 1
@@ -54,15 +57,19 @@ def _evaluate_sequential(agent, num_episodes: int, deterministic: bool, render: 
         lines.append(info.get("lines_cleared", 0))
         combos.append(info.get("max_combo", 0))
     env.close()
-    return _summary(scores, lengths, lines, combos)
+    res = _summary(scores, lengths, lines, combos)
+    if record_actions:
+        res["actions"] = actions
+    return res
 
 
 def evaluate_agent(agent, num_episodes: int = 100, deterministic: bool = True, render: bool = False,
-                   seed: int = 42, max_moves: int = 100_000) -> Dict[str, Any]:
-    """evaluate.py:23-90 (same keys in the returned dict)."""
+                   seed: int = 42, max_moves: int = 100_000, record_actions: bool = False) -> Dict[str, Any]:
+    """evaluate.py:23-90 (same keys in the returned dict).  record_actions: also return every episode's
+    action sequence under "actions" (for replaying the games elsewhere, e.g. through the oracle)."""
     agent.eval()
     if render:
-        return _evaluate_sequential(agent, num_episodes, deterministic, render, seed)
+        return _evaluate_sequential(agent, num_episodes, deterministic, render, seed, record_actions)
     from runtime.device_env import DeviceEnvBatch
 
     dev = agent.device
@@ -77,10 +84,13 @@ def evaluate_agent(agent, num_episodes: int = 100, deterministic: bool = True, r
     rec = torch.zeros((n, 4), dtype=torch.int64, device=dev)  # score, lines, max_combo, done
     info64 = env.info.view(torch.int64).view(n, 7)
     info32 = env.info.view(torch.int32).view(n, 14)
+    log = []
     for step in range(max_moves):
         env.obs(x=x, mask_bits=mb)
         a, _, _ = agent.act_device(x, mb, deterministic=deterministic)
         act.copy_(a)
+        if record_actions:
+            log.append(act.clone())
         env.step(act, want_info=True)
         length += alive.long()
         term = env.terminated.bool() & alive
@@ -93,7 +103,11 @@ def evaluate_agent(agent, num_episodes: int = 100, deterministic: bool = True, r
     out = rec.cpu().numpy()
     lengths = length.cpu().numpy()
     env.close()
-    return _summary(out[:, 0].tolist(), lengths.tolist(), out[:, 1].tolist(), out[:, 2].tolist())
+    res = _summary(out[:, 0].tolist(), lengths.tolist(), out[:, 1].tolist(), out[:, 2].tolist())
+    if record_actions:
+        acts = torch.stack(log).cpu().numpy() if log else np.zeros((0, n), np.int32)
+        res["actions"] = [acts[:int(lengths[e]), e].tolist() for e in range(n)]
+    return res
 
 
 def print_results(results: Dict[str, Any]) -> None:

@@ -67,6 +67,24 @@ RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + 
 RES_GRAD_FUSED = os.environ.get("BB_RES_GRAD_FUSED", "1") != "0"
 
 
+# fp32 (no autocast) 64/128-channel 3x3 convs on csrc/bb_conv32.hip (blocked fp32 chains summed in fp64):
+# the rollout's train-mode forward stays within north_star's 1e-5 of the fp64 network.  By
+# default only where autograd records nothing (the rollout / value forwards); BB_F32_CONV_GRAD=1 also runs
+# the update's forward + data gradient on it.
+F32_CONV = os.environ.get("BB_F32_CONV", "1") != "0"
+F32_CONV_GRAD = os.environ.get("BB_F32_CONV_GRAD", "0") == "1"
+
+
+def _f32_conv_on(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    if not (F32_CONV and x.is_cuda and x.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")):
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad) and not F32_CONV_GRAD:
+        return False
+    from runtime.kernels import conv3x3_f32_fusable
+
+    return conv3x3_f32_fusable(x, conv)
+
+
 def _hip_conv_on(x: torch.Tensor) -> bool:
     return HIP_CONV and x.is_cuda and torch.is_autocast_enabled("cuda") \
         and torch.get_autocast_dtype("cuda") == torch.bfloat16
@@ -83,6 +101,10 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> 
 
         if conv3x3_fusable(x, conv):
             return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox)
+    elif _f32_conv_on(x, conv):
+        from runtime.kernels import Conv3x3F32Function
+
+        return Conv3x3F32Function.apply(x, conv.weight)
     return conv._conv_forward(x, conv.weight, None)
 
 

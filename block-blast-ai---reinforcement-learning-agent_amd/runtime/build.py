@@ -9,7 +9,7 @@ import sys
 from .lib import HOST_LIB_PATH, LIB_PATH, PKG_DIR, REPO_DIR
 
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_nn.hip", "bb_loss.hip", "bb_conv.hip", "bb_optim.hip", "bb_capi.cpp", "bb_tables.cpp"]
+SOURCES = ["bb_env.hip", "bb_ppo.hip", "bb_nn.hip", "bb_loss.hip", "bb_conv.hip", "bb_conv32.hip", "bb_optim.hip", "bb_capi.cpp", "bb_tables.cpp"]
 HEADERS = ["bb_device.h", "bb_solver.h", "bb_env_internal.h", "bb_seed.h"]
 ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
 

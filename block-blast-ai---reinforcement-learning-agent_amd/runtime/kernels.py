@@ -342,6 +342,57 @@ class Conv3x3Function(torch.autograd.Function):
         return dx, dw, None, None
 
 
+_CONV32_PAIRS = ((128, 128), (64, 128))  # forward layers; the 64 -> 128 layer's data gradient runs (128, 64)
+
+
+def conv3x3_f32_fusable(x: torch.Tensor, conv) -> bool:
+    """conv3x3_fusable, fp32 activations and weights, (cin, cout) in _CONV32_PAIRS."""
+    return (x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and conv3x3_fusable(x, conv)
+            and (conv.in_channels, conv.out_channels) in _CONV32_PAIRS)
+
+
+class Conv3x3F32Function(torch.autograd.Function):
+    """conv2d(x, weight, padding=1) without bias in fp32 (no autocast) on csrc/bb_conv32.hip: f32 NHWC
+    activations, every output the fp64 sum of 16-product fp32 MFMA chains rounded once (bb_conv3x3_f32_prep
+    / _forward).  Backward: the data gradient on the same kernel with the tap-reversed, transposed weight
+    image; the weight gradient from aten's convolution_backward (MIOpen)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        _need_cuda(x, weight)
+        x = x.contiguous(memory_format=torch.channels_last)
+        n, cin = x.shape[0], x.shape[1]
+        cout = weight.shape[0]
+        dev = x.device
+        lib = L.load()
+        need_dx = ctx.needs_input_grad[0]
+        wf = torch.empty(9 * cout * cin, dtype=torch.float32, device=dev)
+        wd = torch.empty(9 * cout * cin, dtype=torch.float32, device=dev) if need_dx else None
+        L.check(lib.bb_conv3x3_f32_prep(_p(weight), cin, cout, _w_layout(weight), _p(wf), _p(wd), _s(dev)),
+                "bb_conv3x3_f32_prep")
+        y = torch.empty((n, cout, 8, 8), dtype=torch.float32, device=dev, memory_format=torch.channels_last)
+        L.check(lib.bb_conv3x3_f32_forward(_p(x), _p(wf), n, cin, cout, _p(y), _s(dev)), "bb_conv3x3_f32_forward")
+        ctx.save_for_backward(x, wd, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wd, weight = ctx.saved_tensors
+        n, cin = x.shape[0], x.shape[1]
+        cout = weight.shape[0]
+        dev = x.device
+        dy = dy.float().contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            L.check(L.load().bb_conv3x3_f32_forward(_p(dy), _p(wd), n, cout, cin, _p(dx), _s(dev)),
+                    "bb_conv3x3_f32_forward")
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [False, False, True])[2]
+        return dx, dw
+
+
 class GradMailbox:
     """Hands the identity path's gradient of a ResidualBlock input from
     BatchNormAddReLUFunction.backward to the block's first Conv3x3Function

@@ -35,7 +35,8 @@ extern "C" {
 #define BB_ABI_VERSION 6  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
                               4: bb_conv_in_* and bb_relu_bias_grad* removed;
                               5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed;
-                              6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE */
+                              6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
+                                 bb_conv3x3_f32_prep / _forward */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -381,6 +382,20 @@ int bb_conv3x3_forward_add(const void* d_x, const void* d_w, int32_t N, int32_t 
                            const void* d_add, void* d_y, void* stream);
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
+
+/* The same 3x3 convolutions in fp32 (no autocast: the reference's own precision), for (cin, cout) =
+ * (128, 128), (64, 128) and (128, 64) (the last is the data gradient of the 64 -> 128 layer).  Every output
+ * is the fp64 sum of 16-product fp32 MFMA chains, rounded to fp32 once (csrc/bb_conv32.hip): within
+ * north_star's 1e-5 after the batch-statistics BatchNorms where MIOpen's 1,152-product order was not
+ * (network.py:75-182 in train mode, scripts/train.py:122).  Activations f32 NHWC [N][8][8][C], 16-byte
+ * aligned.  bb_conv3x3_f32_prep writes the f32 weight images d_wf [9][cout][cin] (forward) and
+ * d_wd [9][cin][cout] (taps reversed, data gradient) from w_layout 0 / 1 as bb_conv3x3_prep; either output
+ * may be NULL.  bb_conv3x3_f32_forward writes y = conv(x, w) without bias from d_wf; the data gradient is
+ * the same call on dy with d_wd and cin / cout swapped.  Deterministic. */
+int bb_conv3x3_f32_prep(const float* d_w, int32_t cin, int32_t cout, int32_t w_layout, float* d_wf, float* d_wd,
+                        void* stream);
+int bb_conv3x3_f32_forward(const float* d_x, const float* d_w, int32_t N, int32_t cin, int32_t cout, float* d_y,
+                           void* stream);
 
 /* The end of the PPO minibatch step (PPOAgent.update, ppo.py:400-401):
  * nn.utils.clip_grad_norm_(params, max_norm) followed by

@@ -465,6 +465,75 @@ class Env:
         return self.obs(), reward, terminated, False, self.info(res)
 
 
+    def flat_obs(self):
+        """block_blast_env.py:360-389 ``BlockBlastEnvFlat._get_observation``: board (64, row-major), then per
+        hand slot a 37-wide one-hot of the piece id (all zeros for a used slot), then the 3 used flags as
+        0/1 -- 178 float32 values -- and the int8 action mask."""
+        g = self.engine
+        vals = [float(g.grid[r][c]) for r in range(BOARD) for c in range(BOARD)]
+        for slot in range(HAND):
+            one_hot = [0.0] * len(_PICTURES)
+            if not g.used[slot]:
+                one_hot[g.hand[slot]] = 1.0
+            vals += one_hot
+        vals += [1.0 if u else 0.0 for u in g.used]
+        return {"obs": np.array(vals, dtype=np.float32),
+                "action_mask": g.action_mask().flatten().astype(np.int8)}
+
+
+class ReturnNormalizer:
+    """wrappers.py:144-184 ``NormalizedRewardWrapper`` restated with an independent variance: instead of
+    the reference's incremental Chan update (wrappers.py:187-221) it keeps every discounted return and
+    evaluates the pooled moments of the prior pseudo-sample (count 1e-4, mean 0, variance 1) and all
+    returns from scratch in fp64 with ``math.fsum``.  Equal to the reference's arithmetic up to fp64
+    rounding (tests compare within 1e-12 relative)."""
+
+    PRIOR_COUNT = 1e-4
+
+    def __init__(self, gamma=0.99, epsilon=1e-8):
+        self.gamma, self.epsilon = gamma, epsilon
+        self.returns = 0.0
+        self.history = []
+
+    def variance(self) -> float:
+        import math
+
+        c0, k = self.PRIOR_COUNT, len(self.history)
+        n = c0 + k
+        mean = math.fsum(self.history) / n  # the prior's mean is 0
+        m2 = c0 * 1.0 + c0 * mean * mean + math.fsum((x - mean) ** 2 for x in self.history)
+        return m2 / n
+
+    def step(self, reward: float, done: bool) -> float:
+        """wrappers.py:166-180: returns the normalised reward."""
+        self.returns = self.returns * self.gamma + reward
+        self.history.append(self.returns)
+        out = reward / (self.variance() ** 0.5 + self.epsilon)
+        if done:
+            self.returns = 0.0
+        return out
+
+    def reset(self):
+        self.returns = 0.0  # wrappers.py:182-184 (the statistics persist)
+
+
+class FrameStack:
+    """wrappers.py:224-280 ``FrameStackWrapper``: the last ``num_frames`` boards, oldest first; a reset
+    fills the stack with copies of the first board."""
+
+    def __init__(self, num_frames=4):
+        self.num_frames = num_frames
+        self.frames = None
+
+    def reset(self, board):
+        self.frames = [board.copy() for _ in range(self.num_frames)]
+        return np.stack(self.frames, axis=0)
+
+    def step(self, board):
+        self.frames = self.frames[1:] + [board.copy()]
+        return np.stack(self.frames, axis=0)
+
+
 class VecEnv:
     """wrappers.py:14-141 ``VectorizedBlockBlastEnv`` (sequential loop)."""
 

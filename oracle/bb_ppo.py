@@ -55,6 +55,15 @@ def normalize_advantages(adv):
     return (a - a.mean()) / (a.std() + 1e-8)
 
 
+def categorical_cdf(logits: np.ndarray, mask: np.ndarray) -> np.ndarray:
+    """(N,192) float64 running sums of Categorical(probs=softmax(masked logits)).probs -- the CDF the
+    inverse-CDF sample of masked_categorical walks (network.py:173-180, 213-228); cdf[:, -1] is the total."""
+    lg = torch.from_numpy(np.asarray(logits, dtype=np.float32))
+    mk = torch.from_numpy(np.asarray(mask)).bool()
+    masked = lg + torch.where(mk, torch.zeros_like(lg), torch.full_like(lg, float("-inf")))
+    return np.cumsum(Categorical(probs=F.softmax(masked, dim=-1)).probs.double().numpy(), axis=1)
+
+
 def masked_categorical(logits: np.ndarray, mask: np.ndarray, uniform=None, action=None, deterministic=False):
     """Returns (action int64, log_prob f32, entropy f32) for (N,192) logits."""
     lg = torch.from_numpy(np.asarray(logits, dtype=np.float32))
@@ -66,12 +75,11 @@ def masked_categorical(logits: np.ndarray, mask: np.ndarray, uniform=None, actio
         if deterministic:
             action = torch.argmax(probs, dim=-1)
         else:
-            P = dist.probs.double().numpy()
             u = np.asarray(uniform, dtype=np.float64)
-            cdf = np.cumsum(P, axis=1)
+            cdf = categorical_cdf(logits, mask)
             target = u * cdf[:, -1]
-            out = np.zeros(P.shape[0], dtype=np.int64)
-            for i in range(P.shape[0]):
+            out = np.zeros(cdf.shape[0], dtype=np.int64)
+            for i in range(cdf.shape[0]):
                 hit = np.nonzero((cdf[i] > target[i]) & mk[i].numpy())[0]
                 out[i] = hit[0] if hit.size else np.nonzero(mk[i].numpy())[0][-1]
             action = torch.from_numpy(out)

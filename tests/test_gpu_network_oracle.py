@@ -3,8 +3,9 @@ restatement of the reference network (the rollout's
 ``_raw`` call, network.py:135-182).
 
 ``PPOAgent``'s network in its product configuration (channels_last conv
-stack, HIP BatchNorm + ReLU in train mode, MIOpen convolutions, hipBLASLt
-GEMMs, fp32) and ``oracle.bb_ppo.ReferenceNetwork`` (the reference's plain
+stack, HIP BatchNorm + ReLU in train mode, the fp32 board convolutions of
+csrc/bb_conv32.hip where autograd records nothing and MIOpen's for the input
+layer, hipBLASLt GEMMs, fp32) and ``oracle.bb_ppo.ReferenceNetwork`` (the reference's plain
 modules on the CPU) share their weights; Dropout is 0 on both sides (its mask
 stream cannot be shared).  Inputs: 2,048 states (config 1's minibatch size)
 of C-oracle envs (seeds 42 + i) after 24 synthetic-policy steps, so boards,
@@ -19,19 +20,17 @@ at the same positions.  Train mode is the rollout's mode
 (scripts/train.py:177 keeps the agent in train(): batch statistics); eval mode
 uses the running statistics the train-mode pass left, which are compared too.
 
-Eval mode meets the bound on every element (measured: logits 4.5e-6, values
-2.5e-6).  In train mode the batch-statistics BatchNorms amplify summation-order
-differences: MIOpen's fp32 128-channel convolutions (K = 1,152) accumulate in a
-different order than the CPU's, and tools/diag_net_fp32.py shows the error
-growing in the two residual blocks to 2.7x the CPU's fp32 error (NHWC 9.8e-6
-vs CPU 3.6e-6 after the first; Winograd on or off and the TF32 flags change
-nothing).  Measured: logits 1.28e-5 against the CPU's own 4.0e-6.  So train
-mode asserts what the update test asserts for gradients (test_gpu_ppo_update
-_oracle.py): the GPU's error against the fp64 truth stays within a small
-multiple of the CPU fp32 error (<= 4x, and <= 2e-5 absolute-relative), and at
-most 1 element in 1,000 exceeds 1e-5.
+Both modes meet the bound on every element.  In train mode the batch-statistics BatchNorms amplify
+summation-order differences: with MIOpen's fp32 128-channel convolutions (K = 1,152 products in one
+order) the logits ended 1.28e-5 from the truth (round 4, tools/diag_net_fp32.py, profiles/r04/net/);
+the product now runs those convolutions on csrc/bb_conv32.hip (16-product fp32 MFMA chains summed in
+fp64, rounded once: tests/test_gpu_conv32.py), in every forward autograd does not record (the rollout's
+``_raw``).  The train-mode check also runs at a rollout-sized batch of 16,384 C-oracle states (config 3
+steps 65,536 boards at once; the batch statistics sum over 8x more terms than at 2,048), against the
+same network in float64 on the GPU (the CPU's fp32 is only computed at 2,048).
 """
 import copy
+import functools
 
 import numpy as np
 import pytest
@@ -43,12 +42,13 @@ from oracle import c_oracle as CO
 pytestmark = pytest.mark.gpu
 
 B = 2048
+B_ROLLOUT = 16384
 TOL = 1e-5  # |d| <= TOL * max(1, |truth|)
 
 
-@pytest.fixture(scope="module")
-def states():
-    seeds = np.arange(42, 42 + B, dtype=np.uint64)
+@functools.lru_cache(maxsize=2)
+def _states(n):
+    seeds = np.arange(42, 42 + n, dtype=np.uint64)
     env = CO.CVecEnv(seeds)
     env.reset()
     mask = env.state()["mask"]
@@ -56,8 +56,12 @@ def states():
         mask = env.step(env.random_actions(mask, 0xB10C, t))["mask"]
     st = env.state()
     env.close()
-    boards, pieces, masks = OP.expand_packed(st["board"], st["hand"], st["mask"])
-    return boards, pieces, masks
+    return OP.expand_packed(st["board"], st["hand"], st["mask"])
+
+
+@pytest.fixture(scope="module")
+def states():
+    return _states(B)
 
 
 def _nets(cuda):
@@ -73,23 +77,18 @@ def _nets(cuda):
     return ref, agent
 
 
-TRAIN_RATIO, TRAIN_MAX, TRAIN_FRAC = 4.0, 2e-5, 1e-3  # train mode (docstring)
-
-
-def _check(name, gpu, cpu, truth, strict):
-    """Per-element bound against the fp64 truth for both fp32 results."""
+def _check(name, gpu, cpu, truth):
+    """Per-element bound against the fp64 truth for the GPU's fp32 (and the CPU's, when given)."""
     scale = np.maximum(1.0, np.abs(truth))
     e_gpu = np.abs(gpu.astype(np.float64) - truth) / scale
-    e_cpu = np.abs(cpu.astype(np.float64) - truth) / scale
-    frac = float((e_gpu > TOL).mean())
-    print(f"{name}: max |d|/max(1,|x|) gpu {e_gpu.max():.2e}, cpu fp32 {e_cpu.max():.2e}, "
-          f"|x| max {np.abs(truth).max():.2f}, elements over {TOL:g}: {frac:.1e}")
-    assert e_cpu.max() <= TOL, (name, "the CPU's own fp32 exceeds the bound", e_cpu.max())
-    if strict:
-        assert e_gpu.max() <= TOL, (name, e_gpu.max(), np.unravel_index(e_gpu.argmax(), e_gpu.shape))
-    else:
-        assert e_gpu.max() <= min(TRAIN_MAX, max(TOL, TRAIN_RATIO * e_cpu.max())), (name, e_gpu.max(), e_cpu.max())
-        assert frac <= TRAIN_FRAC, (name, frac)
+    msg = f"{name}: max |d|/max(1,|x|) gpu {e_gpu.max():.2e}"
+    if cpu is not None:
+        e_cpu = np.abs(cpu.astype(np.float64) - truth) / scale
+        msg += f", cpu fp32 {e_cpu.max():.2e}"
+    print(msg + f", |x| max {np.abs(truth).max():.2f}")
+    if cpu is not None:
+        assert e_cpu.max() <= TOL, (name, "the CPU's own fp32 exceeds the bound", e_cpu.max())
+    assert e_gpu.max() <= TOL, (name, e_gpu.max(), np.unravel_index(e_gpu.argmax(), e_gpu.shape))
 
 
 @pytest.mark.parametrize("mode", ["train", "eval"])
@@ -134,5 +133,21 @@ def test_network_forward_matches_reference_fp32(cuda, states, mode):
     np.testing.assert_array_equal(inf_gpu, inf_ref)
     np.testing.assert_array_equal(inf_gpu, masks == 0)
     fin = ~inf_ref
-    _check(f"{mode} logits", lg[fin], lc[fin], l64[fin], strict=mode == "eval")
-    _check(f"{mode} values", vg, vc, v64, strict=mode == "eval")
+    _check(f"{mode} logits", lg[fin], lc[fin], l64[fin])
+    _check(f"{mode} values", vg, vc, v64)
+
+
+def test_network_forward_train_mode_rollout_batch(cuda):
+    """Train mode (batch statistics) at a rollout-sized batch: 16,384 C-oracle states in one forward, every
+    logit and value within 1e-5 * max(1, |x|) of the same network in float64 (on the GPU)."""
+    boards, pieces, masks = _states(B_ROLLOUT)
+    ref, agent = _nets(cuda)
+    net64 = copy.deepcopy(ref).double().to(cuda).train()
+    agent.train()
+    tb, tp = torch.from_numpy(boards).to(cuda), torch.from_numpy(pieces).to(cuda)
+    with torch.no_grad():
+        lg, vg = agent._raw(agent._obs_to_device({"board": boards, "pieces": pieces}))
+        l64, v64 = net64(tb.double(), tp.double())
+    fin = torch.from_numpy(masks).to(cuda).bool()
+    _check(f"train logits B={B_ROLLOUT}", lg[fin].cpu().numpy(), None, l64[fin].cpu().numpy())
+    _check(f"train values B={B_ROLLOUT}", vg.cpu().numpy(), None, v64.cpu().numpy())

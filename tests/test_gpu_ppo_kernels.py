@@ -1,7 +1,8 @@
 """GPU parity of the fused rollout kernels vs the CPU restatement.
 
-masked sample: log-prob / entropy within 1e-5 (fp32, north_star tolerance),
-actions equal for the same uniforms; GAE: bit-exact vs the reference loop in
+masked sample: log-prob / entropy within 1e-5 (fp32, north_star tolerance) on
+every row, actions equal for the same uniforms except on a stated fp32 CDF
+rounding boundary (K_ULP); GAE: bit-exact vs the reference loop in
 numpy float32 (the kernel follows numpy's op order with no FMA contraction);
 gather: exact expansion of packed rollout records.
 """
@@ -21,6 +22,36 @@ def _masks(rng, n, p_valid):
     return m
 
 
+# A sampled index is index work: it must equal the oracle's except where the oracle's target u * sum(P)
+# lies on an fp32 rounding boundary of the CDF.  Bound: each probability of Categorical(softmax) is
+# exp (<= 1 ulp on each side: ocml's expf, Sleef's u10 on the CPU) then two roundings to nearest (the
+# softmax division and Categorical's renormalisation, 0.5 ulp each on each side), so a GPU P_j is within
+# 4 ulps (4 * 2^-24 relative) of the oracle's; the common scale factors cancel in cdf_k / total, so the
+# position of the target relative to a CDF boundary can move by at most 2 x 4 = 8 units of 2^-24 * sum(P)
+# (the fp64 running sums add nothing at this scale).  K_ULP is that 8.
+K_ULP = 8
+
+
+def _check_sampled(logits, mask, u, a, lp, ent, a_ref):
+    """Every sampled action legal; every row where it differs from the oracle's for the same uniform sits
+    on a CDF boundary (|u * sum(P) - cdf[min(a, a_ref)]| <= K_ULP * 2^-24 * sum(P)); log-prob and entropy
+    within 1e-5 of the oracle evaluated at the GPU's action on EVERY row."""
+    n = len(a)
+    assert mask[np.arange(n), a].all()  # only legal actions
+    diff = np.nonzero(a != a_ref)[0]
+    if diff.size:
+        cdf = OP.categorical_cdf(logits[diff], mask[diff])
+        tot = cdf[:, -1]
+        lo = np.minimum(a[diff], a_ref[diff])
+        dist = np.abs(np.asarray(u, np.float64)[diff] * tot - cdf[np.arange(diff.size), lo]) / (tot * 2.0 ** -24)
+        print(f"{diff.size} of {n} sampled actions differ from the oracle; CDF-boundary distance "
+              f"max {dist.max():.2f} x 2^-24 sum(P) (bound {K_ULP})")
+        assert (dist <= K_ULP).all(), (diff[dist > K_ULP], dist[dist > K_ULP])
+    _, lp_at, ent_ref = OP.masked_categorical(logits, mask, action=a)
+    np.testing.assert_allclose(lp, lp_at, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ent, ent_ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("p_valid,scale", [(0.05, 1.0), (0.5, 3.0), (1.0, 10.0), (0.02, 30.0)])
 def test_masked_sample_matches_torch_reference(cuda, p_valid, scale):
     from runtime import kernels as K
@@ -35,10 +66,7 @@ def test_masked_sample_matches_torch_reference(cuda, p_valid, scale):
     mb = K.pack_mask(torch.from_numpy(mask).to(cuda))
     a, lp, ent = K.masked_sample(lg, mb, uniform=torch.from_numpy(u).to(cuda))
     a, lp, ent = a.cpu().numpy(), lp.cpu().numpy(), ent.cpu().numpy()
-    assert mask[np.arange(n), a].all()  # only legal actions
-    assert (a == a_ref).mean() > 0.999
-    same = a == a_ref
-    np.testing.assert_allclose(lp[same], lp_ref[same], rtol=1e-5, atol=1e-5)
+    _check_sampled(logits, mask, u, a, lp, ent, a_ref)
     np.testing.assert_allclose(ent, ent_ref, rtol=1e-5, atol=1e-5)
     # evaluating given actions (PPO update path) and argmax
     _, lp2, _ = K.masked_sample(lg, mb, action_in=torch.from_numpy(a_ref).to(cuda))
@@ -57,9 +85,9 @@ def test_masked_sample_philox_uniform_and_distribution(cuda):
     mask = _masks(rng, n, 0.3)
     u = philox.sample_uniform(n, seed=77, step=5, env_offset=100)
     a_ref, _, _ = OP.masked_categorical(logits, mask, uniform=u)
-    a, _, _ = K.masked_sample(torch.from_numpy(logits).to(cuda), K.pack_mask(torch.from_numpy(mask).to(cuda)),
-                              seed=77, step=5, env_offset=100)
-    assert (a.cpu().numpy() == a_ref).mean() > 0.999
+    a, lp, ent = K.masked_sample(torch.from_numpy(logits).to(cuda), K.pack_mask(torch.from_numpy(mask).to(cuda)),
+                                 seed=77, step=5, env_offset=100)
+    _check_sampled(logits, mask, u, a.cpu().numpy(), lp.cpu().numpy(), ent.cpu().numpy(), a_ref)
     # empirical distribution of one row matches the softmax
     row = np.tile(logits[:1], (200000, 1))
     rm = np.tile(mask[:1], (200000, 1))

@@ -64,3 +64,28 @@ def test_frame_stack_wrapper():
     obs, *_ = env.step(0)
     obs, *_ = env.step(0)
     assert [float(obs["board"][k, 0, 0]) for k in range(3)] == [0.0, 1.0, 2.0]
+
+
+def test_normalized_reward_wrapper_against_independent_variance():
+    """The product's incremental (Chan) variance against the oracle's from-scratch fp64 pooled variance
+    (oracle.bb_game.ReturnNormalizer) over several episodes of a scripted env: the statistics persist
+    across resets, the normalised rewards agree to 1e-12 relative."""
+    import sys
+    import os
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import bb_game as O
+
+    rng = np.random.default_rng(4)
+    env = NormalizedRewardWrapper(_Scripted(list(rng.standard_normal(25) * 3)), gamma=0.99)
+    ora = O.ReturnNormalizer(gamma=0.99)
+    for ep in range(6):
+        env.reset()
+        env.env.rewards = list(rng.standard_normal(int(rng.integers(3, 25))) * (ep + 1))
+        ora.reset()
+        term = False
+        while not term:
+            _, nr, term, _, info = env.step(0)
+            want = ora.step(info["raw_reward"], term)
+            assert abs(nr - want) <= 1e-12 * max(1.0, abs(want)), (ep, nr, want)
+    assert len(ora.history) > 30
