@@ -35,6 +35,7 @@ from .base import BaseAgent
 
 _EPS32 = float(torch.finfo(torch.float32).eps)  # Categorical clamp_probs
 FUSED_ADAM = os.environ.get("BB_FUSED_ADAM", "1") != "0"  # clip_grad_norm_ + Adam on bb_adam_clip_step (GPU)
+DP_OVERLAP_MODES = ("graph-segments", "graph-split", "capture")  # PPOAgent.dp_overlap
 
 
 @dataclass
@@ -299,13 +300,18 @@ class PPOAgent(BaseAgent):
         self.sample_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if sample_seed is None else int(sample_seed)
         self.sample_step = 0
         self._flat_grad = None
-        # data parallelism (world > 1): the flat gradient buffer is all-reduced in buckets of about this many
-        # floats, each launched asynchronously as soon as backward has accumulated its last gradient, so the
-        # RCCL traffic overlaps the rest of the backward pass; "capture" also captures those collectives
-        # inside the optimizer step's HIP graph (one graph per step instead of two around an eager
-        # all-reduce; needs the nccl = RCCL backend, opt-in: unmeasured on an 8-GPU node)
+        # data parallelism (world > 1), dp_overlap (DP_OVERLAP_MODES):
+        #  "graph-segments" (default): backward in two segments cut at the conv stack's output, each its own HIP
+        #    graph: heads + FC backward (graph A1, ~85% of the gradient floats), then the all-reduce of that
+        #    bucket is issued and runs on RCCL's stream while the conv-stack backward (graph A2, ~85% of the
+        #    backward FLOPs) replays; then the conv bucket's all-reduce; then average + clip + Adam (graph B);
+        #  "graph-split": one forward + backward graph, one all-reduce of the whole buffer after it (exposed);
+        #  "capture": the bucketed collectives issued by post-accumulate-grad hooks (buckets of about
+        #    dp_bucket_floats, from the end of the buffer) captured inside one graph per step (nccl = RCCL only)
+        # Eager steps (no graphs) use the same segments in "graph-segments" mode and the hooks otherwise.
         self.dp_bucket_floats = 1 << 21
-        self.dp_overlap = "graph-split"  # or "capture"
+        self.dp_overlap = "graph-segments"
+        self._seg = None  # (conv-stack output, its detached leaf) of the last segmented forward
         self._dp_hooks = None
         self._dp_hooks_on = True  # off while a graph without collectives is captured
         self._dp_works: List[Any] = []
@@ -509,17 +515,57 @@ class PPOAgent(BaseAgent):
         self._dp_works = []
         flat.div_(world)
 
+    def _segmented(self) -> bool:
+        """The data-parallel step runs backward in two segments (dp_overlap "graph-segments")."""
+        return _world() > 1 and self.dp_overlap == "graph-segments" and torch.is_grad_enabled()
+
+    def _dp_split_offset(self) -> int:
+        """Flat-buffer offset where the conv stack's gradients end (they come first: parameter order)."""
+        conv = {id(p) for p in self.network.conv_encoder.parameters()}
+        lay = self._flat_layout
+        split = min(off for p, off, _ in lay if id(p) not in conv)
+        if any(off >= split for p, off, _ in lay if id(p) in conv):
+            raise RuntimeError("conv-stack gradients are not a prefix of the flat buffer")
+        return split
+
     def _minibatch_loss(self, x, masks, actions, old_log_probs, advantages, returns):
         cfg = self.config
-        logits, values = self._raw(x)
+        if self._segmented():
+            self.network.grad_split = []
+            try:
+                logits, values = self._raw(x)
+            finally:
+                cut, self.network.grad_split = self.network.grad_split, None
+            self._seg = cut[0] if len(cut) == 1 else None
+        else:
+            logits, values = self._raw(x)
         if self.fused_loss and logits.is_cuda:  # bb_ppo_loss_forward/backward
             return K.PPOLossFunction.apply(logits, values, masks, actions, old_log_probs, advantages, returns,
                                            cfg.clip_epsilon, cfg.value_coef, cfg.entropy_coef)
         return ppo_loss_torch(logits, values, masks, actions, old_log_probs, advantages, returns, cfg)
 
+    def _backward_segments(self, loss: torch.Tensor, world: int) -> None:
+        """Segmented data-parallel backward: heads + FC, their bucket's all-reduce issued (async), the conv
+        stack's backward while it runs, the conv bucket's all-reduce, then average."""
+        flat = self._grad_buffer()
+        split = self._dp_split_offset()
+        h, hd = self._seg
+        self._seg = None
+        flat.zero_()
+        loss.backward()
+        w_fc = dist.all_reduce(flat[split:], async_op=True)
+        h.backward(hd.grad)
+        w_conv = dist.all_reduce(flat[:split], async_op=True)
+        w_fc.wait()
+        w_conv.wait()
+        flat.div_(world)
+
     def _optimizer_step(self, loss: torch.Tensor) -> None:
         world = _world()
-        if world > 1:  # all-reduce (average) of the flat gradient buffer, bucketed and overlapped with backward
+        if world > 1 and self._seg is not None:
+            self._remove_dp_hooks()
+            self._backward_segments(loss, world)
+        elif world > 1:  # all-reduce (average) of the flat gradient buffer, bucketed and overlapped with backward
             flat = self._grad_buffer()
             flat.zero_()
             self._dp_arm()
@@ -604,7 +650,15 @@ class PPOAgent(BaseAgent):
             if dst.data_ptr() != src.data_ptr():  # minibatch_inputs() buffers are the inputs already
                 dst.copy_(src)
         graphs[0].replay()
-        if len(graphs) > 1:  # the all-reduce of the flat fp32 gradient buffer (RCCL over xGMI), then the step
+        if len(graphs) == 3:  # segments: heads + FC backward, its all-reduce beside the conv-stack backward
+            split = self._dp_split_offset()
+            w_fc = dist.all_reduce(flat[split:], async_op=True)  # RCCL's stream, after graph A1
+            graphs[1].replay()  # the conv-stack backward, concurrent with w_fc
+            w_conv = dist.all_reduce(flat[:split], async_op=True)
+            w_fc.wait()  # the compute stream waits on RCCL's (the host does not block)
+            w_conv.wait()
+            graphs[2].replay()
+        elif len(graphs) == 2:  # the all-reduce of the flat fp32 gradient buffer (RCCL over xGMI), then the step
             work = dist.all_reduce(flat, async_op=True)  # graph B waits on it on the device, the host goes on
             work.wait()
             graphs[1].replay()
@@ -650,7 +704,24 @@ class PPOAgent(BaseAgent):
             del loss
         graphs = [torch.cuda.CUDAGraph()]
         flat = self._flat_grad
-        if world == 1 or self.dp_overlap == "capture":
+        if world > 1 and self.dp_overlap == "graph-segments":
+            flat = self._grad_buffer()
+            self._remove_dp_hooks()
+            graphs += [torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()]
+            with torch.cuda.graph(graphs[0], stream=side):  # A1: zero, forward, loss, heads + FC backward
+                flat.zero_()
+                loss, stats = self._minibatch_loss(*static_in)
+                loss.backward()
+                del loss
+            h, hd = self._seg
+            self._seg = None
+            with torch.cuda.graph(graphs[1], stream=side, pool=graphs[0].pool()):  # A2: conv-stack backward
+                h.backward(hd.grad)
+            del h, hd
+            with torch.cuda.graph(graphs[2], stream=side, pool=graphs[0].pool()):  # B: average, clip, Adam
+                flat.div_(world)
+                self._clip_and_step()
+        elif world == 1 or self.dp_overlap == "capture":
             # one graph per step; data parallel: the bucketed all-reduces issued by the backward hooks are
             # captured with it (RCCL collectives in a HIP graph)
             with torch.cuda.graph(graphs[0], stream=side):

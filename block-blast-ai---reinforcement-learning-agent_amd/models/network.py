@@ -220,6 +220,11 @@ class BlockBlastNetwork(nn.Module):
         self.policy_head = nn.Sequential(nn.Linear(fc_hidden[-1], 256), nn.ReLU(), nn.Linear(256, action_space_size))
         self.value_head = nn.Sequential(nn.Linear(fc_hidden[-1], 128), nn.ReLU(), nn.Linear(128, 1))
         self.apply(self._init_weights)
+        # set to a list by PPOAgent's segmented data-parallel step: the next recorded forward cuts autograd at
+        # the conv stack's output and appends (output, detached leaf), so backward runs in two segments --
+        # heads + FC (which own ~85% of the gradient floats), then the conv stack (which owns ~85% of the
+        # backward's FLOPs) -- with the first segment's all-reduce overlapping the second
+        self.grad_split: Optional[list] = None
 
     @staticmethod
     def _init_weights(m: nn.Module) -> None:
@@ -308,6 +313,10 @@ class BlockBlastNetwork(nn.Module):
     def _trunk(self, x: torch.Tensor):
         """x: (B, 4, 8, 8) -> (fc features (B, fc_hidden[-1]), Linear shadows or None)."""
         h = self.conv_encoder(x, self._conv_images(x))
+        if self.grad_split is not None and torch.is_grad_enabled() and h.requires_grad:
+            hd = h.detach().requires_grad_(True)
+            self.grad_split.append((h, hd))
+            h = hd
         lin0 = self.fc_encoder[0] if len(self.fc_encoder) else None
         if (NHWC_FLATTEN and isinstance(lin0, nn.Linear) and h.is_cuda
                 and h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous()):

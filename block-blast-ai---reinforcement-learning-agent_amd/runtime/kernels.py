@@ -389,7 +389,7 @@ class Conv3x3F32Function(torch.autograd.Function):
                     "bb_conv3x3_f32_forward")
         if ctx.needs_input_grad[1]:
             dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [False, False, True])[2]
+                                                     [False, True, False])[1]
         return dx, dw
 
 

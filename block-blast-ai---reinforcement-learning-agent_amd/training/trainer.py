@@ -25,8 +25,10 @@ samples with minibatch ``batch_size // world`` (``training.minibatch_scope:
 global``, the default: the global minibatch is the reference's) or
 ``batch_size`` (``per_gpu``, SURVEY 8(d) C4: the optimizer steps per update
 are one GPU's); gradients are averaged by an RCCL all-reduce of the flat
-gradient buffer per optimizer step, in buckets issued as backward produces
-them, and advantage moments are global.  BatchNorm statistics stay per rank
+gradient buffer per optimizer step, in two buckets: the heads + FC gradients'
+all-reduce is issued when their backward segment ends and runs while the
+conv stack's backward replays (``training.dp_overlap: graph-segments``, the
+default), and advantage moments are global.  BatchNorm statistics stay per rank
 (documented deviation).
 """
 from __future__ import annotations
@@ -43,7 +45,7 @@ import torch
 import torch.distributed as dist
 import yaml
 
-from agents.ppo import PackedRolloutBuffer, PPOAgent, PPOConfig, broadcast_parameters
+from agents.ppo import DP_OVERLAP_MODES, PackedRolloutBuffer, PPOAgent, PPOConfig, broadcast_parameters
 from runtime.device_env import DeviceEnvBatch
 from utils.device import get_device, set_seed
 from utils.logger import Logger, MetricsTracker, TensorBoardLogger
@@ -262,9 +264,16 @@ def train(config: Dict[str, Any], resume_path: Optional[str] = None, seed: int =
     if scope not in ("global", "per_gpu"):
         raise ValueError(f"training.minibatch_scope must be 'global' or 'per_gpu', got {scope!r}")
     local_batch = agent_cfg.batch_size if scope == "per_gpu" else max(1, agent_cfg.batch_size // world)
-    # data-parallel gradient all-reduce: "graph-split" (two graphs around the bucketed all-reduce) or
-    # "capture" (the collectives captured in the step's graph; nccl = RCCL only)
-    agent.dp_overlap = str(train_cfg.get("dp_overlap", "graph-split"))
+    # data-parallel gradient all-reduce (agents.ppo.DP_OVERLAP_MODES): "graph-segments" (default:
+    # the heads + FC bucket's all-reduce overlaps the conv-stack backward), "graph-split" (one exposed
+    # all-reduce between two graphs) or "capture" (the collectives inside the step's graph; nccl = RCCL only)
+    overlap = str(train_cfg.get("dp_overlap", "graph-segments"))
+    if overlap not in DP_OVERLAP_MODES:
+        raise ValueError(f"training.dp_overlap must be one of {DP_OVERLAP_MODES}, got {overlap!r}")
+    if overlap == "capture" and world > 1 and dist.get_backend() != "nccl":
+        raise ValueError("training.dp_overlap 'capture' puts the collectives inside a HIP graph: it needs the nccl "
+                         f"(RCCL) backend, this run uses {dist.get_backend()!r}")
+    agent.dp_overlap = overlap
     # BASELINE config 5: the rollout step captured in a HIP graph (training.graph_rollout)
     graph_rollout = bool(train_cfg.get("graph_rollout", False)) and device.type == "cuda"
 

@@ -1,7 +1,9 @@
 """Worker for test_gpu_train.py's data-parallel graph test (torch.distributed.run,
 2 ranks sharing the card over gloo): the HIP-graph-replayed data-parallel
 optimizer step (forward + backward graph, all-reduce, clip + Adam graph) against
-the eager data-parallel step on the same per-rank minibatches."""
+the eager data-parallel step on the same per-rank minibatches, for dp_overlap "graph-segments" (three graphs:
+heads + FC backward, conv-stack backward beside the first bucket's all-reduce, clip + Adam) and "graph-split"
+(two graphs around one all-reduce)."""
 import json
 import os
 import sys
@@ -39,28 +41,36 @@ def main():
     dist.init_process_group("gloo")
     rank = dist.get_rank()
     cuda = torch.device("cuda", 0)
-    res = {}
-    for graphs in (True, False):
-        torch.manual_seed(0)
-        agent = PPOAgent(PPOConfig(batch_size=512), device=cuda, sample_seed=1)
-        agent.use_graphs = graphs
-        agent.train()
-        for m in agent.network.modules():
-            if isinstance(m, torch.nn.Dropout):
-                m.p = 0.0
-        stats = []
-        for batch in _batches(rank):
-            stats.append(agent.train_minibatch(*(t.to(cuda) for t in batch)).clone())
-        torch.cuda.synchronize()
-        flat = torch.cat([p.detach().double().reshape(-1).cpu() for p in agent.network.parameters()])
-        res[graphs] = (flat, torch.stack(stats).double().cpu())
-        if graphs:
-            assert len(agent._graphs) == 1 and len(next(iter(agent._graphs.values()))[0]) == 2
-    (fg, sg), (fe, se) = res[True], res[False]
-    rel = float((fg - fe).norm() / fe.norm())
+    report = {}
+    for mode, ngraphs in (("graph-segments", 3), ("graph-split", 2)):
+        res = {}
+        for graphs in (True, False):
+            torch.manual_seed(0)
+            agent = PPOAgent(PPOConfig(batch_size=512), device=cuda, sample_seed=1)
+            agent.dp_overlap = mode
+            agent.use_graphs = graphs
+            agent.train()
+            for m in agent.network.modules():
+                if isinstance(m, torch.nn.Dropout):
+                    m.p = 0.0
+            stats = []
+            for batch in _batches(rank):
+                stats.append(agent.train_minibatch(*(t.to(cuda) for t in batch)).clone())
+            torch.cuda.synchronize()
+            flat = torch.cat([p.detach().double().reshape(-1).cpu() for p in agent.network.parameters()])
+            res[graphs] = (flat, torch.stack(stats).double().cpu())
+            if graphs:
+                assert len(agent._graphs) == 1 and len(next(iter(agent._graphs.values()))[0]) == ngraphs
+        (fg, sg), (fe, se) = res[True], res[False]
+        rel = float((fg - fe).norm() / fe.norm())
+        report[mode] = {"checksum": float(fg.sum()), "checksum_eager": float(fe.sum()), "weights_rel": rel,
+                        "weights_maxabs": float((fg - fe).abs().max()),
+                        "stats_maxabs": float((sg - se).abs().max()), "flat": fg}
+    # the two modes compute the same step: segmented and unsegmented weights agree
+    a, b = report["graph-segments"].pop("flat"), report["graph-split"].pop("flat")
+    report["modes_rel"] = float((a - b).norm() / b.norm())
     with open(os.path.join(out, f"graph_rank{rank}.json"), "w") as f:
-        json.dump({"checksum": float(fg.sum()), "checksum_eager": float(fe.sum()), "weights_rel": rel,
-                   "weights_maxabs": float((fg - fe).abs().max()), "stats_maxabs": float((sg - se).abs().max())}, f)
+        json.dump(report, f)
     dist.barrier()
     dist.destroy_process_group()
 

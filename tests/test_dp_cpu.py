@@ -37,11 +37,12 @@ def _agent():
     return agent
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="graph-split"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     agent = _agent()
+    agent.dp_overlap = mode
     agent.dp_bucket_floats = 1 << 19  # several buckets over the 5.29 M gradient floats
     full = _data(world * B)
     mine = tuple(t[rank * B:(rank + 1) * B] for t in full)
@@ -58,10 +59,22 @@ def _worker(rank, world, port, q):
         orig_clip()
 
     agent._dp_finish, agent._clip_and_step = finish, clip
+    if mode == "graph-segments":  # record the order: FC bucket issued before the conv-stack backward ran
+        calls = []
+        real_ar = dist.all_reduce
+
+        def all_reduce(t, *a, **k):
+            calls.append(("all_reduce", t.numel(), agent.network.conv_encoder[0].weight.grad is not None
+                          and bool(agent.network.conv_encoder[0].weight.grad.abs().sum() > 0)))
+            return real_ar(t, *a, **k)
+
+        import agents.ppo as P
+        P.dist.all_reduce = all_reduce
     loss, _ = agent._minibatch_loss(*mine)
     agent._optimizer_step(loss)
     # the reference: one process, the concatenated minibatch, plain autograd
     ref = _agent()
+    ref.dp_overlap = "graph-split"  # plain autograd: no segment cut in the reference's forward
     ref_loss, _ = ref._minibatch_loss(*full)
     params = [p for p in ref.network.parameters() if p.requires_grad]
     grads = torch.autograd.grad(ref_loss, params)
@@ -71,11 +84,38 @@ def _worker(rank, world, port, q):
         err = max(err, float((got - g).abs().max()))
         scale = max(scale, float(g.abs().max()))
     w = torch.cat([p.detach().reshape(-1) for p in agent.network.parameters()])
+    if mode == "graph-segments":
+        P.dist.all_reduce = real_ar
+        # two buckets: the heads + FC one issued before any conv-stack gradient existed, then the conv one
+        split = agent._dp_split_offset()
+        n = agent._flat_grad.numel()
+        ok = [c[1] for c in calls] == [n - split, split] and calls[0][2] is False and calls[1][2] is True
+        seen["buckets"], seen["issued_in_backward"] = (2, 2) if ok else (len(calls), -1)
     q.put((rank, seen["buckets"], seen["issued_in_backward"], err, scale, float(w.double().sum())))
     dist.destroy_process_group()
 
 
+def test_segmented_backward_equals_concatenated_minibatch():
+    """dp_overlap "graph-segments" (the default) in its eager form: backward cut at the conv stack's output,
+    the heads + FC bucket all-reduced before the conv-stack backward runs, then the conv bucket; the averaged
+    gradient equals the concatenated minibatch's and the replicas stay identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29200 + (os.getpid() % 500)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, "graph-segments")) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, nb, issued, err, scale, _ in res:
+        assert nb == 2 and issued == 2, (rank, nb, issued)
+        assert err <= 1e-5 * scale + 1e-7, (rank, err, scale)
+    assert res[0][5] == pytest.approx(res[1][5], rel=0, abs=0)
+
+
 def test_bucketed_allreduce_equals_concatenated_minibatch():
+    """dp_overlap "graph-split" / "capture" in their eager form: the post-accumulate-grad hooks' buckets."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + (os.getpid() % 500)

@@ -103,8 +103,10 @@ def test_data_parallel_two_ranks_stay_in_lockstep(cuda, tmp_path, scope, steps):
 
 
 def test_data_parallel_graph_step_equals_eager(cuda, tmp_path):
-    """Data parallel keeps HIP-graph replay: forward + backward into the flat
-    gradient buffer (graph 1), the all-reduce, average + clip + Adam (graph 2).
+    """Data parallel keeps HIP-graph replay.  "graph-segments" (default): forward + heads/FC backward (graph
+    1), their bucket's all-reduce beside the conv-stack backward (graph 2), the conv bucket's all-reduce,
+    average + clip + Adam (graph 3); "graph-split": forward + backward into the flat gradient buffer
+    (graph 1), the all-reduce, average + clip + Adam (graph 2).
     Two ranks (gloo, one card), six minibatches each: the replicas stay in
     lockstep and the weights / statistics equal the eager data-parallel step's
     (MIOpen in deterministic mode, so both runs sum in the same order)."""
@@ -116,8 +118,11 @@ def test_data_parallel_graph_step_equals_eager(cuda, tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = [json.loads((tmp_path / f"graph_rank{k}.json").read_text()) for k in range(2)]
     print(res)
-    assert res[0]["checksum"] == res[1]["checksum"]  # lockstep (graphed)
-    assert res[0]["checksum_eager"] == res[1]["checksum_eager"]  # lockstep (eager)
-    for d in res:
-        assert d["weights_rel"] < 1e-6 and d["weights_maxabs"] < 1e-6, d
-        assert d["stats_maxabs"] < 1e-5, d
+    for mode in ("graph-segments", "graph-split"):
+        r0, r1 = res[0][mode], res[1][mode]
+        assert r0["checksum"] == r1["checksum"], mode  # lockstep (graphed)
+        assert r0["checksum_eager"] == r1["checksum_eager"], mode  # lockstep (eager)
+        for d in (r0, r1):
+            assert d["weights_rel"] < 1e-6 and d["weights_maxabs"] < 1e-6, (mode, d)
+            assert d["stats_maxabs"] < 1e-5, (mode, d)
+    assert res[0]["modes_rel"] < 1e-6 and res[1]["modes_rel"] < 1e-6, res
