@@ -554,7 +554,8 @@ class PPOAgent(BaseAgent):
         flat.zero_()
         loss.backward()
         w_fc = dist.all_reduce(flat[split:], async_op=True)
-        h.backward(hd.grad)
+        with K.deferred_wgrad(self.device):  # joined before the conv bucket's all-reduce
+            h.backward(hd.grad)
         w_conv = dist.all_reduce(flat[:split], async_op=True)
         w_fc.wait()
         w_conv.wait()
@@ -576,7 +577,8 @@ class PPOAgent(BaseAgent):
             self._remove_dp_hooks()
             for p in self.network.parameters():
                 p.grad = None
-            loss.backward()
+            with K.deferred_wgrad(self.device):  # conv weight gradients beside the rest of the backward
+                loss.backward()
         self._clip_and_step()
 
     def _fused_clip_adam(self) -> bool:
@@ -716,7 +718,8 @@ class PPOAgent(BaseAgent):
             h, hd = self._seg
             self._seg = None
             with torch.cuda.graph(graphs[1], stream=side, pool=graphs[0].pool()):  # A2: conv-stack backward
-                h.backward(hd.grad)
+                with K.deferred_wgrad(self.device):
+                    h.backward(hd.grad)
             del h, hd
             with torch.cuda.graph(graphs[2], stream=side, pool=graphs[0].pool()):  # B: average, clip, Adam
                 flat.div_(world)
@@ -737,7 +740,8 @@ class PPOAgent(BaseAgent):
                 with torch.cuda.graph(graphs[0], stream=side):
                     flat.zero_()
                     loss, stats = self._minibatch_loss(*static_in)
-                    loss.backward()
+                    with K.deferred_wgrad(self.device):
+                        loss.backward()
                     del loss
             finally:
                 self._dp_hooks_on = True

@@ -7,10 +7,18 @@
 // forward and 200 us backward per layer at N = 2048 (bf16), about a third of a
 // PPO minibatch step, and the convolution bias cost a separate add forward and
 // a reduction backward; these kernels are HBM passes:
-//   forward : u = x + conv_bias[c] (optional) -> per-channel sum / sum of
-//             squares -> normalise, scale, shift, optional ReLU, saved mean /
-//             inverse std, running-stat update (momentum, unbiased variance),
-//             exactly nn.BatchNorm2d's training forward of conv(x) + bias;
+//   forward : per-channel sum / sum of squares of x, accumulated in fp64 from
+//             the first add -> normalise, scale, shift, optional ReLU, saved mean
+//             / inverse std, running-stat update (momentum, unbiased variance),
+//             exactly nn.BatchNorm2d's training forward of u = conv(x) + bias.
+//             The bias only shifts the batch mean, so it cancels in the output:
+//             the output is (x - mean_x) * invstd * w + b with mean_x the mean of
+//             x itself (one rounding, no u = x + bias rounding amplified by the
+//             normalisation) and mean_u = mean_x + bias (fp64) feeds the running
+//             mean; the saved mean is mean_x.  A one-pass fp32 sum of squares
+//             loses the variance to cancellation when |mean| >> std (the fp32
+//             train-mode logits ended 1.2e-5 from the fp64 network with it,
+//             tests/test_gpu_network_oracle.py);
 //   backward: per-channel sum(g), sum(g * xhat), sum(xhat) with g = dy masked
 //             by the ReLU (recomputed from x) -> dx, dweight, dbias and the
 //             convolution bias gradient sum(dx).
@@ -23,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <math.h>
+
+#include <type_traits>
 
 #include "bb_env_internal.h"
 
@@ -95,7 +105,8 @@ struct ChanCoef {
 __device__ __forceinline__ ChanCoef coef_of(int c, const float* pre_bias, const float* mean, const float* invstd,
                                             const float* w, const float* b, bool bwd) {
   ChanCoef k;
-  k.pb = pre_bias ? pre_bias[c] : 0.f;
+  (void)pre_bias;  // the statistics are those of x: the bias cancels (see the top of the file)
+  k.pb = 0.f;
   k.mu = bwd ? mean[c] : 0.f;
   k.is = bwd ? invstd[c] : 0.f;
   k.sc = bwd ? k.is * w[c] : 0.f;
@@ -103,18 +114,22 @@ __device__ __forceinline__ ChanCoef coef_of(int c, const float* pre_bias, const 
   return k;
 }
 
-// One element's contribution: forward (u, u^2, 0); backward (g, g*xhat, xhat).
+// One element's contribution: forward (x, x^2, 0) in fp64; backward (g, g*xhat, xhat) in f32.
 template <bool BWD>
-__device__ __forceinline__ void accumulate(float xv, float gv, const ChanCoef& k, int relu, float& s, float& q,
-                                           float& t) {
-  const float u = xv + k.pb;
-  if (BWD) {
+using Acc = typename std::conditional<BWD, float, double>::type;
+
+template <bool BWD>
+__device__ __forceinline__ void accumulate(float xv, float gv, const ChanCoef& k, int relu, Acc<BWD>& s, Acc<BWD>& q,
+                                           Acc<BWD>& t) {
+  if constexpr (BWD) {
+    const float u = xv + k.pb;
     const float g = (relu && (u - k.mu) * k.sc + k.sh <= 0.f) ? 0.f : gv;  // the forward's exact ops
     const float xh = (u - k.mu) * k.is;
     s += g;
     q += g * xh;
     t += xh;
   } else {
+    const double u = (double)xv;
     s += u;
     q += u * u;
   }
@@ -141,7 +156,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
   const int rows_per_iter = kBnThreads / cpr;
   const int r = threadIdx.x / cpr, kk = threadIdx.x % cpr;
   const ChanCoef k = coef_of(c, pre_bias, mean, invstd, w, b, BWD);
-  float s = 0.f, q = 0.f, t = 0.f;
+  Acc<BWD> s = 0, q = 0, t = 0;
   if (r < rows_per_iter) {
     for (int n = blockIdx.y * rows_per_iter + r; n < N; n += gridDim.y * rows_per_iter) {
       const int64_t i = ((int64_t)n * C + c) * cpr + kk;
@@ -175,12 +190,13 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
                                                              const float* __restrict__ invstd, int relu,
                                                              double* __restrict__ part) {
   constexpr int V = Vec<T>::N;
-  __shared__ float red[kQ][kBnThreads * V];
+  constexpr int NQ = BWD ? kQ : 2;  // the forward has no third quantity
+  __shared__ Acc<BWD> red[NQ][kBnThreads * V];
   const int cpr = C / V;
   const int rows_per_iter = kBnThreads / cpr;
   const int r = threadIdx.x / cpr, kc = threadIdx.x % cpr;
   ChanCoef k[V];
-  float s[V], q[V], t[V];
+  Acc<BWD> s[V], q[V], t[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     k[j] = coef_of(kc * V + j, pre_bias, mean, invstd, w, b, BWD);
@@ -208,14 +224,14 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
   for (int j = 0; j < V; ++j) {
     red[0][threadIdx.x * V + j] = s[j];
     red[1][threadIdx.x * V + j] = q[j];
-    red[2][threadIdx.x * V + j] = t[j];
+    if (BWD) red[NQ - 1][threadIdx.x * V + j] = t[j];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += kBnThreads) {
     const int cc = c / V, jc = c % V;
     double a[kQ] = {0.0, 0.0, 0.0};
     for (int rr = 0; rr < rows_per_iter; ++rr)
-      for (int m = 0; m < kQ; ++m) a[m] += red[m][(rr * cpr + cc) * V + jc];
+      for (int m = 0; m < NQ; ++m) a[m] += (double)red[m][(rr * cpr + cc) * V + jc];
     for (int m = 0; m < kQ; ++m) part[((int64_t)blockIdx.x * C + c) * kQ + m] = a[m];
   }
 }
@@ -268,17 +284,18 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_fwd(const double* __re
   int c;
   double a[kQ];
   if (!channel_sums(part, nb, C, c, a)) return;
-  const double m = a[0] / M;
+  const double m = a[0] / M;  // mean of x (the bias-free input)
   double var = a[1] / M - m * m;
   if (var < 0.0) var = 0.0;
   const float mu = (float)m, is = (float)(1.0 / sqrt(var + (double)eps));
   save_mean[c] = mu;
   save_invstd[c] = is;
-  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+  const float mu_u = (float)(m + (pre_bias ? (double)pre_bias[c] : 0.0));  // the mean of u = x + bias
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu_u;
   if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1.0 ? var * M / (M - 1.0) : var);
   if (nbt && c == 0) nbt[0] += 1;
   float4* o = reinterpret_cast<float4*>(coef + kCoef * c);
-  o[0] = make_float4(pre_bias ? pre_bias[c] : 0.f, mu, is * w[c], b[c]);
+  o[0] = make_float4(0.f, mu, is * w[c], b[c]);
 }
 
 // Backward finalisation: dweight = sum(g * xhat), dbias = sum(g), the
@@ -302,7 +319,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_bwd(const double* __re
   if (db) db[c] = (float)sg;
   if (dpb) dpb[c] = (float)((double)sc * (sg - M * (double)mg) - (double)sc * (double)mgx * sx);
   float4* o = reinterpret_cast<float4*>(coef + kCoef * c);
-  o[0] = make_float4(pre_bias ? pre_bias[c] : 0.f, mean[c], sc, b[c]);
+  o[0] = make_float4(0.f, mean[c], sc, b[c]);  // mean[c]: the forward's saved mean of x (bias-free)
   o[1] = make_float4(is, mg, mgx, 0.f);
 }
 

@@ -267,6 +267,67 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 _CONV_CH = (64, 128)
 
+# ---------------------------------------------------------------------------
+# Deferred convolution weight gradients: inside ``deferred_wgrad(device)`` the
+# board convolutions' weight-gradient kernels run on a side stream forked from
+# the current one and accumulate into ``weight.grad`` there, off autograd's
+# critical path (dgrad -> BatchNorm backward -> dgrad ...): the MFMA-bound
+# weight gradients overlap the HBM-bound BatchNorm passes of the rest of the
+# backward.  On exit the current stream waits for the side stream, so every
+# weight gradient is complete before anything after the block reads it
+# (clip + Adam, the data-parallel all-reduce).  Captured HIP graphs record the
+# fork / join.  Outside the block the weight gradient is autograd's as usual.
+# ---------------------------------------------------------------------------
+ASYNC_WGRAD = os.environ.get("BB_ASYNC_WGRAD", "1") != "0"
+_wg_streams = {}
+_wg_active = {}  # device -> [depth, used]
+
+
+class deferred_wgrad:
+    def __init__(self, device: torch.device, enabled: bool = True):
+        self.dev = torch.device(device)
+        self.on = bool(enabled and ASYNC_WGRAD and self.dev.type == "cuda")
+
+    def __enter__(self):
+        if self.on:
+            st = _wg_active.setdefault(self.dev, [0, False])
+            st[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            st = _wg_active[self.dev]
+            st[0] -= 1
+            if st[1]:
+                torch.cuda.current_stream(self.dev).wait_stream(_wg_streams[self.dev])
+                st[1] = st[0] > 0
+        return False
+
+
+def _wgrad_deferred(weight: torch.Tensor, dev: torch.device, saved, compute) -> bool:
+    """Run compute() -> dw on the side stream and add it into weight.grad there when a deferred_wgrad block
+    is open on ``dev``; False (nothing done) otherwise.  ``saved``: tensors of the current stream that the
+    side stream reads (kept from reuse until it has)."""
+    st = _wg_active.get(dev)
+    if not st or st[0] <= 0 or weight.grad is not None and weight.grad.is_sparse:
+        return False
+    side = _wg_streams.get(dev)
+    if side is None:
+        side = _wg_streams[dev] = torch.cuda.Stream(dev)
+    cur = torch.cuda.current_stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        dw = compute()
+        g = weight.grad
+        if g is None:
+            weight.grad = dw
+        else:
+            g.add_(dw)
+    for t in saved:
+        t.record_stream(side)
+    st[1] = True
+    return True
+
 
 def conv3x3_fusable(x: torch.Tensor, conv) -> bool:
     """An nn.Conv2d 3x3 / stride 1 / pad 1 with 64 or 128 channels in and out,
@@ -335,10 +396,16 @@ class Conv3x3Function(torch.autograd.Function):
             nbytes = lib.bb_conv3x3_workspace_bytes(n, cin, cout)
             if nbytes < 0:
                 raise L.BBNativeError(f"bb_conv3x3_workspace_bytes rejected {n}x{cin}->{cout}")
-            ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
-            dw = torch.empty_like(weight, dtype=torch.float32)
-            L.check(lib.bb_conv3x3_wgrad(_p(x), _p(dy), n, cin, cout, _p(ws), _w_layout(dw), _p(dw), _s(dev)),
-                    "bb_conv3x3_wgrad")
+
+            def wgrad():
+                ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+                g = torch.empty_like(weight, dtype=torch.float32)
+                L.check(lib.bb_conv3x3_wgrad(_p(x), _p(dy), n, cin, cout, _p(ws), _w_layout(g), _p(g), _s(dev)),
+                        "bb_conv3x3_wgrad")
+                return g
+
+            if not _wgrad_deferred(weight, dev, (x, dy), wgrad):
+                dw = wgrad()
         return dx, dw, None, None
 
 
@@ -388,8 +455,12 @@ class Conv3x3F32Function(torch.autograd.Function):
             L.check(L.load().bb_conv3x3_f32_forward(_p(dy), _p(wd), n, cout, cin, _p(dx), _s(dev)),
                     "bb_conv3x3_f32_forward")
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1]
+            def wgrad():
+                return torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
+                                                           [0, 0], 1, [False, True, False])[1]
+
+            if not _wgrad_deferred(weight, dev, (x, dy), wgrad):
+                dw = wgrad()
         return dx, dw
 
 

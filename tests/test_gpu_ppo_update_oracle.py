@@ -174,8 +174,11 @@ def _oracle_forced(net, buf, last, cfg, perm, snaps, per_gpu):
                 # a noisy tensor's small gradient elements are normalised by Adam to ~±lr whatever their size,
                 # so their summation-order differences reach the update at full weight (measured up to 1.2e-2 on
                 # the first convolution's weight, run to run with MIOpen's atomic split-K weight gradient); the
-                # per-element bound above (a tenth of one Adam step) holds for every tensor
-                assert rl <= (3e-2 if noisy else 1e-2), (k, name, "update rel L2", rl)
+                # per-element bound above (a tenth of one Adam step) holds for every tensor.  The looser bound
+                # applies to that tensor alone (the 4 -> 64 input convolution, whose weight gradient is
+                # MIOpen's split-K with atomics); any other noisy tensor keeps 1e-2
+                first_conv = name == "conv_encoder.0.weight"
+                assert rl <= (3e-2 if noisy and first_conv else 1e-2), (k, name, "update rel L2", rl)
 
     means, per, adv, ret = OP.ppo_update(ref, opt, buf, last, cfg, perm, before_step=before, after_step=after)
     return means, per, adv, ret, worst
