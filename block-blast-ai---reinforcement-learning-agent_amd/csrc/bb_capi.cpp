@@ -844,6 +844,18 @@ extern "C" int bb_conv3x3_f32_forward(const float* d_x, const float* d_w, int32_
   return BB_OK;
 }
 
+extern "C" int bb_linear_f32(const float* d_x, const float* d_w, const float* d_bias, int32_t M, int32_t N, int32_t K,
+                             float* d_y, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % 32)
+    return fail(nullptr, BB_ERR_ARG, "bb_linear_f32: M, N, K must be positive, N % 128 == 0, K % 32 == 0");
+  if (!d_x || !d_w || !d_y) return fail(nullptr, BB_ERR_ARG, "bb_linear_f32: NULL argument");
+  if (!al16(d_x) || !al16(d_w) || !al16(d_y))
+    return fail(nullptr, BB_ERR_ARG, "bb_linear_f32: tensors must be 16-byte aligned");
+  hipError_t st = launch_linear_f32(d_x, d_w, d_bias, M, N, K, d_y, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_f32");
+  return BB_OK;
+}
+
 static_assert(BB_OPT_MAX_TENSORS == kOptMaxTensors, "bbvec.h / bb_env_internal.h tensor-table size");
 
 extern "C" int64_t bb_adam_clip_workspace_bytes(int32_t num_tensors, const int64_t* h_numel) {

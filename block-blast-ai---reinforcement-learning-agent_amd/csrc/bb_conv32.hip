@@ -1,5 +1,5 @@
-// bb_conv32.hip -- the CNN's 3x3 / pad-1 convolutions on 8x8 boards in fp32 (gfx950), accumulated so that
-// the result is as close to the exact sum as one fp32 rounding allows.
+// bb_conv32.hip -- the CNN's 3x3 / pad-1 convolutions on 8x8 boards and its long-K Linear layer in fp32
+// (gfx950), accumulated so that the result is as close to the exact sum as one fp32 rounding allows.
 //
 // The policy's fp32 forward (network.py:75-117, ResidualBlock network.py:14-30) runs in training mode in the
 // rollout (scripts/train.py:122 keeps agent.train(): batch-statistics BatchNorm after every convolution).
@@ -197,6 +197,114 @@ __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __
   }
 }
 
+// ---------------------------------------------------------------------------
+// y[m][n] = sum_k x[m][k] w[n][k] + bias[n] in fp32 with the same accumulation (nn.Linear's forward,
+// network.py:89-117: the first fc_encoder layer has K = 8,192, where hipBLASLt's fp32 order cost more than
+// north_star's 1e-5 at the logits after the batch-statistics BatchNorms, tools/diag_net_fp32.py).  Every
+// output is the fp64 sum of 16-product fp32 MFMA chains plus the bias, rounded once.  x [M][K], w [N][K]
+// row-major (K contiguous), y [M][N]; N % 128 == 0, K % 32 == 0.  Workgroup: 4 waves, 64 rows x 128 columns;
+// waves 2 (m) x 2 (n) of 32 x 64; stages of 32 k through a 2-slot LDS ring (direct global -> LDS copies),
+// rows of 128 bytes XOR-swizzled by chunk ^ ((row >> 1) & 7).
+// ---------------------------------------------------------------------------
+constexpr int kL32Threads = 256;
+constexpr int kL32BM = 64, kL32BN = 128, kL32BK = 32;
+
+__global__ void __launch_bounds__(kL32Threads) linear32_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ y, int M, int N, int K) {
+  constexpr int ABYTES = kL32BM * kL32BK * 4, BBYTES = kL32BN * kL32BK * 4;
+  constexpr int SBYTES = ABYTES + BBYTES;
+  constexpr int NW = kL32Threads / 64;
+  constexpr int TM = 2, TN = 4;  // 16 x 16 tiles per wave: 32 m x 64 n
+  __shared__ __attribute__((aligned(16))) uint8_t sm[2 * SBYTES];
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * kL32BM, n0 = blockIdx.y * kL32BN;
+  const int NS = K / kL32BK;
+  auto stage = [&](int st) {
+    uint8_t* a = sm + (st & 1) * SBYTES;
+    uint8_t* b = a + ABYTES;
+    const int k0 = st * kL32BK;
+#pragma unroll
+    for (int kq = 0; kq < ABYTES / 1024 / NW; ++kq) {
+      const int kk = wid + kq * NW, e = kk * 64 + lane, r = e / 8, lc = (e % 8) ^ ((r >> 1) & 7);
+      const int row = min(m0 + r, M - 1);  // rows past M read the last one (never stored)
+      c32_glds16(x + (size_t)row * K + k0 + lc * 4, a + kk * 1024);
+    }
+#pragma unroll
+    for (int kq = 0; kq < BBYTES / 1024 / NW; ++kq) {
+      const int kk = wid + kq * NW, e = kk * 64 + lane, r = e / 8, lc = (e % 8) ^ ((r >> 1) & 7);
+      c32_glds16(w + (size_t)(n0 + r) * K + k0 + lc * 4, b + kk * 1024);
+    }
+  };
+  stage(0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  const int wm = (wid & 1) * 32, wn = (wid >> 1) * 64;
+  double dacc[TN][TM][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dacc[j][i][e] = 0.0;
+  for (int st = 0; st < NS; ++st) {
+    if (st + 1 < NS) stage(st + 1);  // its slot was last read in stage st - 1, before that stage's barrier
+    const uint8_t* a = sm + (st & 1) * SBYTES;
+    const uint8_t* b = a + ABYTES;
+#pragma unroll
+    for (int kb = 0; kb < kL32BK / 16; ++kb) {
+      f32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm + 16 * i + r16;
+        af[i] = *reinterpret_cast<const f32x4*>(a + r * 128 + (((4 * kb + g) ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn + 16 * j + r16;
+        bf[j] = *reinterpret_cast<const f32x4*>(b + r * 128 + (((4 * kb + g) ^ ((r >> 1) & 7)) << 4));
+      }
+      f32x4 acc[TN][TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[j][s4], af[i][s4], acc[j][i], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dacc[j][i][e] += (double)acc[j][i][e];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  // D[n = wn + 16 j + 4 g + e][m = wm + 16 i + r16]: 4 consecutive outputs of one row = one 16-byte store
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm + 16 * i + r16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn + 16 * j + 4 * g;
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (float)(dacc[j][i][e] + (bias ? (double)bias[n + e] : 0.0));
+      *reinterpret_cast<f32x4*>(y + (size_t)m * N + n) = f32x4{o[0], o[1], o[2], o[3]};
+    }
+  }
+}
+
 template <int CIN, int COUT>
 hipError_t c32_fwd_t(const float* x, const float* w, int nb, float* y, hipStream_t s) {
   hipLaunchKernelGGL((conv32_fwd_kernel<CIN, COUT>), dim3((nb + kC32Boards - 1) / kC32Boards), dim3(kC32Threads), 0,
@@ -222,6 +330,14 @@ hipError_t launch_conv3x3_f32_forward(const float* x, const float* w, int nb, in
   if (cin == 64) return c32_fwd_t<64, 128>(x, w, nb, y, s);
   if (cout == 64) return c32_fwd_t<128, 64>(x, w, nb, y, s);
   return c32_fwd_t<128, 128>(x, w, nb, y, s);
+}
+
+hipError_t launch_linear_f32(const float* x, const float* w, const float* bias, int M, int N, int K, float* y,
+                             hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || N % kL32BN || K % kL32BK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(linear32_kernel, dim3((M + kL32BM - 1) / kL32BM, N / kL32BN), dim3(kL32Threads), 0, s, x, w,
+                     bias, y, M, N, K);
+  return hipGetLastError();
 }
 
 }  // namespace bb

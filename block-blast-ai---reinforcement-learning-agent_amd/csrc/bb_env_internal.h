@@ -125,6 +125,8 @@ bool conv3x3_f32_supported(int cin, int cout);
 hipError_t launch_conv3x3_f32_prep(const float* w, int cin, int cout, int wl, float* wf, float* wd, hipStream_t s);
 hipError_t launch_conv3x3_f32_forward(const float* x, const float* w, int nb, int cin, int cout, float* y,
                                       hipStream_t s);
+hipError_t launch_linear_f32(const float* x, const float* w, const float* bias, int M, int N, int K, float* y,
+                             hipStream_t s);
 
 int64_t ppo_loss_workspace_bytes(int B);
 hipError_t launch_ppo_loss_forward(const float* logits, const float* values, const float* mask, const int64_t* actions,

@@ -85,6 +85,22 @@ def _f32_conv_on(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return conv3x3_f32_fusable(x, conv)
 
 
+def _linear(x: torch.Tensor, lin: nn.Linear, weight: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """lin(x) (``weight`` replaces lin.weight: the permuted first FC weight).  In the same fp32 forwards as the
+    fp32 convolutions (no autocast, nothing recorded for autograd) it runs on bb_linear_f32, whose blocked
+    fp32 chains summed in fp64 keep the K = 8,192 first layer's sums within one rounding (hipBLASLt's order
+    cost the rollout's logits more than north_star's 1e-5, tools/diag_net_fp32.py)."""
+    w = lin.weight if weight is None else weight
+    if (F32_CONV and x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 2
+            and not torch.is_autocast_enabled("cuda")
+            and not (torch.is_grad_enabled() and (x.requires_grad or w.requires_grad))
+            and w.shape[0] % 128 == 0 and w.shape[1] % 32 == 0):
+        from runtime.kernels import linear_f32
+
+        return linear_f32(x, w, lin.bias)
+    return F.linear(x, w, lin.bias)
+
+
 def _hip_conv_on(x: torch.Tensor) -> bool:
     return HIP_CONV and x.is_cuda and torch.is_autocast_enabled("cuda") \
         and torch.get_autocast_dtype("cuda") == torch.bfloat16
@@ -291,6 +307,8 @@ class BlockBlastNetwork(nn.Module):
                     i += 2
                     continue
                 z = F.linear(z, *sh[m])
+            elif isinstance(m, nn.Linear):
+                z = _linear(z, m)
             else:
                 z = m(z)
             i += 1
@@ -341,7 +359,7 @@ class BlockBlastNetwork(nn.Module):
             if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
                 wp = wp.to(torch.bfloat16, memory_format=torch.contiguous_format)  # autocast's cast + the permute, one pass
             w = wp.reshape(o, hh * ww * c)
-            return self._run(self.fc_encoder, F.linear(flat, w, lin0.bias), None, skip_first=True), None
+            return self._run(self.fc_encoder, _linear(flat, lin0, w), None, skip_first=True), None
         sh = self._linear_shadows(h, None)
         return self._run(self.fc_encoder, h.reshape(h.shape[0], -1), sh), sh
 

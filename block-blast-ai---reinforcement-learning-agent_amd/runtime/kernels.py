@@ -464,6 +464,19 @@ class Conv3x3F32Function(torch.autograd.Function):
         return dx, dw
 
 
+def linear_f32(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """nn.Linear's forward in fp32 with blocked fp32 MFMA chains summed in fp64 (bb_linear_f32); no autograd."""
+    _need_cuda(x, weight)
+    x = x.contiguous()
+    weight = weight.contiguous()
+    m, k = x.shape
+    n = weight.shape[0]
+    y = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    L.check(L.load().bb_linear_f32(_p(x), _p(weight), _p(bias.contiguous() if bias is not None else None), m, n, k,
+                                   _p(y), _s(x.device)), "bb_linear_f32")
+    return y
+
+
 class GradMailbox:
     """Hands the identity path's gradient of a ResidualBlock input from
     BatchNormAddReLUFunction.backward to the block's first Conv3x3Function

@@ -156,6 +156,7 @@ SIGNATURES = {
     "bb_conv3x3_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _P, _P]),
     "bb_conv3x3_f32_prep": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "bb_conv3x3_f32_forward": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
+    "bb_linear_f32": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),
     "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
     "bb_ppo_loss_backward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),

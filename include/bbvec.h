@@ -36,7 +36,7 @@ extern "C" {
                               4: bb_conv_in_* and bb_relu_bias_grad* removed;
                               5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed;
                               6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
-                                 bb_conv3x3_f32_prep / _forward */
+                                 bb_conv3x3_f32_prep / _forward, bb_linear_f32 */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -396,6 +396,12 @@ int bb_conv3x3_f32_prep(const float* d_w, int32_t cin, int32_t cout, int32_t w_l
                         void* stream);
 int bb_conv3x3_f32_forward(const float* d_x, const float* d_w, int32_t N, int32_t cin, int32_t cout, float* d_y,
                            void* stream);
+/* nn.Linear's forward y = x w^T + bias in fp32 with the same accumulation (fp64 sum of 16-product fp32 MFMA
+ * chains, the bias added in fp64, one rounding): the K = 8,192 first fc_encoder layer of the rollout's
+ * forward (network.py:89-117, 135-182).  x [M][K], w [N][K] (nn.Linear.weight), y [M][N], all row-major and
+ * 16-byte aligned; bias [N] or NULL; N % 128 == 0, K % 32 == 0.  Deterministic. */
+int bb_linear_f32(const float* d_x, const float* d_w, const float* d_bias, int32_t M, int32_t N, int32_t K,
+                  float* d_y, void* stream);
 
 /* The end of the PPO minibatch step (PPOAgent.update, ppo.py:400-401):
  * nn.utils.clip_grad_norm_(params, max_norm) followed by

@@ -130,3 +130,27 @@ def test_conv32_function_autograd(cuda):
     for got, want in ((xg.grad, x64.grad), (wg.grad, w64.grad)):
         rel = float((got.double() - want).norm() / want.norm())
         assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 128, 32), (77, 512, 8192), (2048, 512, 8192), (300, 256, 512), (64, 128, 256)])
+def test_linear_f32_within_error_bound(cuda, m, n, k):
+    """bb_linear_f32 (nn.Linear forward) against float64: |y - y64| <= 2^-24 |y64| + gamma_16 sum|x w| (+ the
+    bias, added in fp64 before the one rounding); ragged M; its RMS error not above hipBLASLt's fp32 at K >= 512."""
+    from runtime.kernels import linear_f32
+
+    g = torch.Generator().manual_seed(m + n + k)
+    x = (torch.randn(m, k, generator=g).relu() * 1.7).to(cuda)
+    w = (torch.randn(n, k, generator=g) * (2.0 / k) ** 0.5).to(cuda)
+    b = (torch.randn(n, generator=g) * 0.1).to(cuda)
+    y = linear_f32(x, w, b)
+    y64 = x.double() @ w.double().t() + b.double()
+    absum = x.double().abs() @ w.double().abs().t()
+    err = (y.double() - y64).abs()
+    lim = 2.0 ** -24 * y64.abs() + 16 * 2.0 ** -24 * absum
+    assert bool((err <= lim).all()), float((err / lim).max())
+    yb = torch.nn.functional.linear(x, w, b)
+    ours, blas = _rms_rel(y, y64, absum), _rms_rel(yb, y64, absum)
+    print(f"linear {m}x{k}->{n}: max err / bound {float((err / lim).max()):.3f}; RMS ours {ours:.2e}, hipBLASLt {blas:.2e}")
+    if k >= 512 and m >= 64:
+        assert ours <= blas, (ours, blas)
+    assert torch.equal(y, linear_f32(x, w, b))
