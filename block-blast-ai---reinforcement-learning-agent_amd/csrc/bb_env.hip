@@ -896,6 +896,10 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
 #ifndef BB_ASYNC_LINEONLY
 #define BB_ASYNC_LINEONLY 0  // search waves: slow_phase_wave's line-only second order (BB_SLOW_LINE_MIN tasks up)
 #endif
+#ifndef BB_SEARCH_QUOTA
+// search waves: the quota pass schedule (gen_hands_quota, bb_solver.h); 0: gen_hands_multi's packed passes
+#define BB_SEARCH_QUOTA 1
+#endif
 #ifndef BB_ASYNC_PHILOX_EARLY
 #define BB_ASYNC_PHILOX_EARLY 0  // the policy uniform computed at the top of every iteration (every lane)
 #endif
@@ -995,8 +999,13 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
 #if BB_ASYNC_DIAG_DUPSEARCH
         const Pcg rng_dup = rng;
 #endif
+#if BB_SEARCH_QUOTA
+        gen_hands_quota<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
+                                                     a.pack_next, lds, dprof_p, 0, release);
+#else
         gen_hands_multi<64, (bool)BB_ASYNC_LINEONLY>(req, B, rng, ids, t.row, t.d, jt, lane, a.pack_first,
                                                      a.pack_next, lds, dprof_p, 0, release);
+#endif
 #if BB_ASYNC_DIAG_DUPSEARCH
         {  // diagnostics only: the same search once more, results dropped (its instructions are the search
            // waves' share of the kernel's SQ counts: counts of this build minus the shipped build's)

@@ -908,4 +908,217 @@ __device__ __forceinline__ void gen_hands_multi(uint64_t parked, uint64_t eB, Pc
 #undef BB_MT
 }
 
+// ---------------------------------------------------------------------------
+// gen_hands_multi with a quota pass schedule (round 5).  Same contract and same result (the earliest
+// successful attempt of every env, every earlier attempt of it proven unsolvable; 100 attempts -> the
+// last draw), different order of work.  gen_hands_multi packs the leading attempt lanes whose level-1
+// slots fit kMultiPasses passes and tests all of their slots: a solvable attempt has ~50-75 slots but
+// succeeds on its first ~1.3 (tools/search_stats.c), so a pass was spent on one attempt's slots while
+// other envs' first attempts waited for the next round's draws.  Here every pass deals each ACTIVE
+// attempt lane (valid, not yet successful, slots left, its env undecided and no earlier attempt of its
+// env successful) at most `quota` of its next untested slots (kQuota in the round's first pass, then up
+// to 64), attempt-major, until the 64 slot lanes are full; an env is decided once it has a successful
+// attempt whose earlier attempts are all complete, or all of its attempts are complete.  Every round
+// ends with every env decided, so it advances either to its accepted attempt or past all its drawn
+// ones.  tools/search_quota_model.c (bench workload, 7 envs per call): 1.04 rounds and 2.2 passes per
+// call against 1.68 and 3.0 for the packed schedule, -23% modelled search cycles.
+// ---------------------------------------------------------------------------
+#ifndef BB_QUOTA_FIRST
+#define BB_QUOTA_FIRST 4
+#endif
+#ifndef BB_QUOTA_NEXT
+#define BB_QUOTA_NEXT 64
+#endif
+
+template <int kEnvs, bool kLineOnly = false, typename Release = NoRelease>
+__device__ __forceinline__ void gen_hands_quota(uint64_t parked, uint64_t eB, Pcg& rng, uint32_t& ids,
+                                                const PieceRow* tbl, const uint8_t* dtab, const JumpRow* J,
+                                                int lane, int pack_first, int pack_next, uint32_t* lds,
+                                                uint64_t* prof = nullptr, int att0 = 0,
+                                                const Release& release = Release()) {
+#define BB_MT(x) const uint64_t x = prof ? __builtin_amdgcn_s_memtime() : 0
+  const int me = lane % kEnvs;
+  int att = att0;
+  uint32_t last_ids = 0;
+  uint64_t todo = parked;
+  int pk = pack_first < kPack ? pack_first : kPack;
+#pragma unroll 1
+  while (todo) {
+    BB_MT(p0);
+    const int E = __popcll(todo);
+    int K = 64 / E;
+    K = K < pk ? K : pk;
+    K = K < kPack ? K : kPack;
+    K = K > 1 ? K : 1;
+    const int nl = E * K;
+    const int k = (int)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)E));
+    const int es = lane - k * E;
+    const int e = select_bit(todo, (uint32_t)es);
+    Pcg s0;
+    s0.hi = __shfl(rng.hi, e);
+    s0.lo = __shfl(rng.lo, e);
+    s0.inc_hi = __shfl(rng.inc_hi, e);
+    s0.inc_lo = __shfl(rng.inc_lo, e);
+    s0.buf = __shfl(rng.buf, e);
+    s0.has = __shfl((int)rng.has, e) != 0;
+    const uint64_t B = __shfl(eB, e);
+    const int a0 = __shfl(att, e);
+    const bool valid = lane < nl && a0 + k < kMaxAttempts;
+    uint32_t e_ids = 0;
+    Pcg e_after = s0;
+    bool rej = false;
+    if (valid) rej = draw_attempt_jump(s0, J, k, e_ids, e_after);
+    if (__ballot(rej)) {  // rare Lemire rejection: the lowest env on the exact sequential path
+      const int e0 = __ffsll((unsigned long long)todo) - 1;
+      Pcg w;
+      w.hi = __shfl(rng.hi, e0);
+      w.lo = __shfl(rng.lo, e0);
+      w.inc_hi = __shfl(rng.inc_hi, e0);
+      w.inc_lo = __shfl(rng.inc_lo, e0);
+      w.buf = __shfl(rng.buf, e0);
+      w.has = __shfl((int)rng.has, e0) != 0;
+      uint32_t wids = (uint32_t)__shfl((int)last_ids, e0);
+      gen_hand_wave(__shfl(eB, e0), w, wids, __shfl(att, e0), tbl, dtab, J, lane, pk, pack_next, lds);
+      if (me == e0) {
+        rng = w;
+        ids = wids;
+      }
+      release(me == e0);
+      todo &= todo - 1;
+      continue;
+    }
+    BB_MT(p1);
+    uint64_t eA0 = 0ull, eA1 = 0ull, eA2 = 0ull;
+    if (valid) {
+      eA0 = anchors_of(tbl[hand_id(e_ids, 0)], B);
+      eA1 = anchors_of(tbl[hand_id(e_ids, 1)], B);
+      eA2 = anchors_of(tbl[hand_id(e_ids, 2)], B);
+    }
+    const int S = valid ? __popcll(eA0) + __popcll(eA1) + __popcll(eA2) : 0;
+    const uint64_t vmask = __ballot(valid);
+    uint64_t every = 1ull;  // bits 0, E, 2E, ...: the attempt lanes of env slot 0
+    for (int w = E; w < 64; w <<= 1) every |= every << w;
+    const uint64_t envl = lane < E ? (every << lane) & vmask : 0ull;  // lanes of env slot `lane` (lane < E)
+    int done = 0;           // this attempt lane's slots tested so far
+    uint64_t okm = 0ull;    // attempt lanes with a successful slot
+    BB_MT(p2);
+    uint64_t pq = 0, ps = 0;
+#pragma unroll 1
+    for (int pass = 0;; ++pass) {
+      // env decisions (lanes < E, env slot = lane): decided by its earliest success with every earlier
+      // attempt complete, or by all of its attempts complete
+      const uint64_t complete = __ballot(valid && done >= S) | ~vmask;
+      bool undecided = false;
+      if (lane < E) {
+        const uint64_t okl = okm & envl;
+        const uint64_t prior = okl ? envl & ((okl & (0ull - okl)) - 1ull) : envl;
+        undecided = (prior & ~complete) != 0ull;
+      }
+      const uint64_t und = __ballot(undecided);  // bit es: env slot es undecided
+      if (!und) break;
+      BB_MT(q0);
+      // this attempt lane's share of the pass: its env undecided, no success of its env at or before it
+      const uint64_t jenv_all = every << es;  // lanes of my env slot
+      const bool blocked = (okm & jenv_all & ((2ull << lane) - 1ull)) != 0ull;
+      const bool act = valid && done < S && ((und >> es) & 1ull) && !blocked;
+      const int cap = pass == 0 ? BB_QUOTA_FIRST : BB_QUOTA_NEXT;
+      int c = act ? (S - done < cap ? S - done : cap) : 0;
+      const int incl0 = (int)wave_incl_add((uint32_t)c);
+      const int off = incl0 - c;
+      c = off >= 64 ? 0 : (off + c > 64 ? 64 - off : c);  // the pass holds 64 slots
+      const int total = __builtin_amdgcn_readlane(incl0, 63) < 64 ? __builtin_amdgcn_readlane(incl0, 63) : 64;
+      // owner j of slot lane `lane`: the last attempt lane whose first slot of the pass is <= it
+      wave_lds_fence();
+      lds[lane] = 0u;
+      wave_lds_fence();
+      if (c > 0) atomicMax(&lds[off], (uint32_t)lane);
+      wave_lds_fence();
+      const int j = (int)wave_incl_max(lds[lane]);
+      const uint32_t jid = __shfl(e_ids, j);
+      const uint64_t jA0 = __shfl(eA0, j), jA1 = __shfl(eA1, j), jA2 = __shfl(eA2, j);
+      const uint64_t jB = __shfl(B, j);
+      const int jrem0 = __shfl(done - off, j) + lane;  // slot index within attempt j
+      int q = 0;
+      uint64_t B1 = 0, A2 = 0, A3 = 0;
+      uint32_t bi = 0, ci = 0;
+      {  // every lane computes its slot (lanes past `total` a dummy one) and drops it by select
+        const int c0 = __popcll(jA0), c1 = __popcll(jA1);
+        const int f = jrem0 < c0 ? 0 : (jrem0 < c0 + c1 ? 1 : 2);
+        const uint64_t Af = f == 0 ? jA0 : (f == 1 ? jA1 : jA2);
+        const int rem = jrem0 - (f == 0 ? 0 : (f == 1 ? c0 : c0 + c1));
+        const int p = select_bit(Af, (uint32_t)rem) & 63;
+        bi = hand_id(jid, f == 0 ? 1 : 0);
+        ci = hand_id(jid, f == 2 ? 1 : 2);
+        B1 = clear_full(jB | (tbl[hand_id(jid, f)].shape << p));
+        q = pair_quick_bf(B1, tbl[bi], tbl[ci], dtab[bi * kPieces + ci], A2, A3);
+        if (lane >= total) q = 0;
+      }
+      // attempt lane L owns the pass's slot bits [off, off + c)
+      const uint64_t own = c > 0 ? (c == 64 ? ~0ull : ((1ull << c) - 1ull)) << off : 0ull;
+      const uint64_t qam = __ballot((__ballot(q == 1) & own) != 0ull);
+      const uint64_t jenv = every << (j % E);
+      bool ok = q == 1;
+      const bool need = q == 2 && !((qam | okm) & jenv & ((2ull << j) - 1ull));
+      BB_MT(q1);
+      if (__ballot(need))
+        ok |= slow_phase_wave<kLineOnly>(need, B1, bi, ci, A2, A3, tbl, lane, lds,
+                                         (uint32_t)((j % E) << 8 | (j / E)));
+      BB_MT(q2);
+      pq += q1 - q0;
+      ps += q2 - q1;
+      okm |= __ballot((__ballot(ok) & own) != 0ull);
+      done += c;
+    }
+    BB_MT(p3);
+    // resolve every env of the round in its own lanes: its earliest successful attempt, else past all
+    // of its (complete, failed) attempts
+    const bool mine = (todo >> me) & 1ull;
+    const int my_es = __popcll(todo & ((1ull << me) - 1ull));
+    const uint64_t em = mine ? (every << my_es) & vmask : 0ull;
+    const uint64_t hit = em & okm;
+    int src = -1;
+    if (hit) src = __ffsll((unsigned long long)hit) - 1;
+    else if (em) src = 63 - __clzll((long long)em);
+    const int from = src < 0 ? lane : src;
+    const uint32_t f_ids = __shfl(e_ids, from);
+    Pcg fa;
+    fa.hi = __shfl(e_after.hi, from);
+    fa.lo = __shfl(e_after.lo, from);
+    fa.buf = __shfl(e_after.buf, from);
+    fa.has = __shfl((int)e_after.has, from) != 0;
+    bool fin = false;
+    if (src >= 0) {
+      rng.hi = fa.hi;
+      rng.lo = fa.lo;
+      rng.buf = fa.buf;
+      rng.has = fa.has;
+      if (hit) {
+        ids = f_ids;
+        fin = true;
+      } else {
+        att += __popcll(em);
+        last_ids = f_ids;
+        if (att >= kMaxAttempts) {
+          ids = last_ids;
+          fin = true;
+        }
+      }
+    }
+    todo &= ~(__ballot(fin && lane < kEnvs) & (kEnvs >= 64 ? ~0ull : ((1ull << (kEnvs & 63)) - 1ull)));
+    release(fin && lane < kEnvs);
+    pk = pack_next > 0 ? pack_next : 2 * pk;
+    pk = pk < kPack ? pk : kPack;
+    if (prof) {
+      BB_MT(p4);
+      prof[0] += p1 - p0;
+      prof[1] += p2 - p1;
+      prof[2] += pq;
+      prof[3] += ps;
+      prof[4] += (p3 - p2) - pq - ps;
+      prof[5] += p4 - p3;
+    }
+  }
+#undef BB_MT
+}
+
 }  // namespace bb

@@ -23,6 +23,12 @@ VARIANTS = {
     # the round-3 compile-time variants measured slower were removed (tools/patches/r03_compile_variants.diff
     # restores them), so their A/B arms cannot be rebuilt from this tree.
     "main": [],
+    # round 5: search waves' pass schedule -- 0: gen_hands_multi's packed passes (round 4); quota per attempt
+    # in a round's first pass (shipped 4) and later passes (shipped 64)
+    "mq0": ["-DBB_SEARCH_QUOTA=0"],
+    "q2": ["-DBB_QUOTA_FIRST=2"],
+    "q8": ["-DBB_QUOTA_FIRST=8"],
+    "qn16": ["-DBB_QUOTA_NEXT=16"],
     # bb_rollout (rollout_async_kernel): search waves per workgroup, their priority, in-lane quick-test slots
     "asw3": ["-DBB_ASYNC_SW=3"],
     "asw5": ["-DBB_ASYNC_SW=5"],
