@@ -618,6 +618,10 @@ __global__ void __launch_bounds__(kEscBlock) escalate_kernel(EnvDev e, const Pie
 }
 
 // ---------------------------------------------------------------------------
+#ifndef BB_STEP_QUOTA
+// bb_step's in-wave searches (step_fused_kernel): the quota pass schedule too (0: packed passes)
+#define BB_STEP_QUOTA 0
+#endif
 // bb_step in one launch: step_fused_kernel.  Two lanes per env (32 envs per
 // wave): lanes l and l + 32 both hold env l.  Copy 1 idles through the move
 // and the finalize and takes the post-move board and the drawn pieces from
@@ -741,7 +745,11 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
   const uint64_t parked = __ballot(park) & kEnvMask;
   if (parked) {
     uint32_t ids = 0;
+#if BB_STEP_QUOTA
+    gen_hands_quota<kE, true>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+#else
     gen_hands_multi<kE, true>(parked, s.B, s.rng, ids, t.row, t.d, jt, lane, a.pack_first, a.pack_next, lds);
+#endif
     if ((parked >> (lane % kE)) & 1ull) s.hand = ids | ((uint32_t)s.rng.has << 22);
   }
   // ---- finalize (copy 0): game over, reward, outputs, auto-reset, mask, policy

@@ -29,6 +29,7 @@ VARIANTS = {
     "q2": ["-DBB_QUOTA_FIRST=2"],
     "q8": ["-DBB_QUOTA_FIRST=8"],
     "qn16": ["-DBB_QUOTA_NEXT=16"],
+    "sq1": ["-DBB_STEP_QUOTA=1"],
     # bb_rollout (rollout_async_kernel): search waves per workgroup, their priority, in-lane quick-test slots
     "asw3": ["-DBB_ASYNC_SW=3"],
     "asw5": ["-DBB_ASYNC_SW=5"],
