@@ -114,13 +114,15 @@ __device__ __forceinline__ ChanCoef coef_of(int c, const float* pre_bias, const 
   return k;
 }
 
-// One element's contribution: forward (x, x^2, 0) in fp64; backward (g, g*xhat, xhat) in f32.
-template <bool BWD>
-using Acc = typename std::conditional<BWD, float, double>::type;
+// One element's contribution: forward (x, x^2, 0), for f32 activations in fp64 from the first add (the fp32
+// rollout forward's precision, tests/test_gpu_network_oracle.py), for bf16 ones in f32 per thread as in
+// round 4 (the bf16 training step's activations carry 8 bits); backward (g, g*xhat, xhat) in f32.
+template <typename T, bool BWD>
+using Acc = typename std::conditional<BWD || !std::is_same<T, float>::value, float, double>::type;
 
-template <bool BWD>
-__device__ __forceinline__ void accumulate(float xv, float gv, const ChanCoef& k, int relu, Acc<BWD>& s, Acc<BWD>& q,
-                                           Acc<BWD>& t) {
+template <typename T, bool BWD>
+__device__ __forceinline__ void accumulate(float xv, float gv, const ChanCoef& k, int relu, Acc<T, BWD>& s,
+                                           Acc<T, BWD>& q, Acc<T, BWD>& t) {
   if constexpr (BWD) {
     const float u = xv + k.pb;
     const float g = (relu && (u - k.mu) * k.sc + k.sh <= 0.f) ? 0.f : gv;  // the forward's exact ops
@@ -129,7 +131,7 @@ __device__ __forceinline__ void accumulate(float xv, float gv, const ChanCoef& k
     q += g * xh;
     t += xh;
   } else {
-    const double u = (double)xv;
+    const Acc<T, BWD> u = (Acc<T, BWD>)xv;
     s += u;
     q += u * u;
   }
@@ -156,7 +158,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
   const int rows_per_iter = kBnThreads / cpr;
   const int r = threadIdx.x / cpr, kk = threadIdx.x % cpr;
   const ChanCoef k = coef_of(c, pre_bias, mean, invstd, w, b, BWD);
-  Acc<BWD> s = 0, q = 0, t = 0;
+  Acc<T, BWD> s = 0, q = 0, t = 0;
   if (r < rows_per_iter) {
     for (int n = blockIdx.y * rows_per_iter + r; n < N; n += gridDim.y * rows_per_iter) {
       const int64_t i = ((int64_t)n * C + c) * cpr + kk;
@@ -164,7 +166,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
       Vec<T>::load(x, i, fx);
       if (BWD) Vec<T>::load(dy, i, fg);
 #pragma unroll
-      for (int j = 0; j < V; ++j) accumulate<BWD>(fx[j], BWD ? fg[j] : 0.f, k, relu, s, q, t);
+      for (int j = 0; j < V; ++j) accumulate<T, BWD>(fx[j], BWD ? fg[j] : 0.f, k, relu, s, q, t);
     }
   }
   const double v[kQ] = {wave_sum((double)s), wave_sum((double)q), wave_sum((double)t)};
@@ -191,12 +193,12 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
                                                              double* __restrict__ part) {
   constexpr int V = Vec<T>::N;
   constexpr int NQ = BWD ? kQ : 2;  // the forward has no third quantity
-  __shared__ Acc<BWD> red[NQ][kBnThreads * V];
+  __shared__ Acc<T, BWD> red[NQ][kBnThreads * V];
   const int cpr = C / V;
   const int rows_per_iter = kBnThreads / cpr;
   const int r = threadIdx.x / cpr, kc = threadIdx.x % cpr;
   ChanCoef k[V];
-  Acc<BWD> s[V], q[V], t[V];
+  Acc<T, BWD> s[V], q[V], t[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     k[j] = coef_of(kc * V + j, pre_bias, mean, invstd, w, b, BWD);
@@ -217,7 +219,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
     for (int u = 0; u < kUnroll<BWD>; ++u) {
       if (n0 + u * stride >= R) break;
 #pragma unroll
-      for (int j = 0; j < V; ++j) accumulate<BWD>(fx[u][j], BWD ? fg[u][j] : 0.f, k[j], relu, s[j], q[j], t[j]);
+      for (int j = 0; j < V; ++j) accumulate<T, BWD>(fx[u][j], BWD ? fg[u][j] : 0.f, k[j], relu, s[j], q[j], t[j]);
     }
   }
 #pragma unroll
