@@ -278,7 +278,10 @@ _CONV_CH = (64, 128)
 # (clip + Adam, the data-parallel all-reduce).  Captured HIP graphs record the
 # fork / join.  Outside the block the weight gradient is autograd's as usual.
 # ---------------------------------------------------------------------------
-ASYNC_WGRAD = os.environ.get("BB_ASYNC_WGRAD", "1") != "0"
+# opt-in: measured slower (bf16 optimizer step 1.885 ms with the side stream against 1.711 ms without, two
+# interleaved repeats each, profiles/r05/pu/): the weight gradients and the BatchNorm backward passes slow each other
+# down more than the overlap saves (bn_reduce_nhwc backward 21 -> 35 us, conv_wgrad 38 -> 46 us per call)
+ASYNC_WGRAD = os.environ.get("BB_ASYNC_WGRAD", "0") == "1"
 _wg_streams = {}
 _wg_active = {}  # device -> [depth, used]
 
