@@ -294,6 +294,7 @@ int main(int argc, char** argv) {
   int Ecall = argc > 3 ? atoi(argv[3]) : 7;
   int Q = argc > 4 ? atoi(argv[4]) : 8;
   int Qn = argc > 5 ? atoi(argv[5]) : 64;
+  if (argc > 6) g_noleaf = atoi(argv[6]);
   init_bits();
   uint64_t* seeds = malloc(sizeof(uint64_t) * n);
   for (int i = 0; i < n; ++i) seeds[i] = 42 + (uint64_t)i;
