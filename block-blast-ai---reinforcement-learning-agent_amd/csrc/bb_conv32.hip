@@ -41,8 +41,12 @@ constexpr int kC32Threads = 512;
 constexpr int kC32Boards = 2;
 constexpr int kC32Rows = kC32Boards * 64;
 constexpr int kC32Zero = 16;
-constexpr int kC32Sci = 32;  // input channels per weight stage
-constexpr int kC32Ring = 2;
+#ifndef BB_CONV32_SCI
+#define BB_CONV32_SCI 32  // input channels per weight stage of the 128-input-channel layers (32 or 64)
+#endif
+#ifndef BB_CONV32_RING
+#define BB_CONV32_RING 2  // weight-stage LDS ring slots (stages copied RING - 1 ahead)
+#endif
 #ifndef BB_CONV32_BLOCK
 #define BB_CONV32_BLOCK 16  // channels per fp32 MFMA chain before the fp64 add (16 or 32)
 #endif
@@ -50,6 +54,18 @@ constexpr int kC32Ring = 2;
 __device__ __forceinline__ void c32_glds16(const void* g, uint8_t* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
+
+// The same copy from inline asm: the compiler does not track it, so it inserts no vmcnt(0) before the LDS reads of
+// the current stage while later stages' copies are in flight; counted waits (C32_WAIT_VM) cover it.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else in these kernels keeps it live
+__device__ __forceinline__ void c32_glds16_async(const void* g, uint8_t* lds_base) {
+  const uint32_t l = (uint32_t)(size_t)((__attribute__((address_space(3))) uint8_t*)lds_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+// s_waitcnt with vmcnt = n and lgkmcnt = 0 (expcnt not waited)
+#define C32_WAIT_VM_LGKM0(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (7 << 4) | (((n) >> 4) << 14))
 
 __global__ void __launch_bounds__(256) conv32_prep_kernel(const float* __restrict__ w, int cout, int cin, int wl,
                                                           float* __restrict__ wf, float* __restrict__ wd) {
@@ -63,6 +79,13 @@ __global__ void __launch_bounds__(256) conv32_prep_kernel(const float* __restric
   if (wd) wd[((8 - t) * cin + ci) * cout + co] = v;
 }
 
+template <int CIN>
+constexpr int c32_sci() { return CIN == 128 ? BB_CONV32_SCI : 32; }
+template <int SCI>
+__device__ __forceinline__ int c32_wkey(int co) {  // weight rows of 8 chunks (two per bank line) or 16 (one)
+  return SCI == 64 ? (co & 15) : ((co >> 1) & 7);
+}
+
 template <int CIN, int COUT>
 __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w, float* __restrict__ y,
@@ -70,9 +93,12 @@ __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __
   constexpr int RB = CIN * 4;                       // bytes per pixel row
   constexpr int NCH = CIN / 4;                      // 16-byte chunks per pixel row (16 or 32)
   constexpr int XBYTES = (kC32Rows + kC32Zero) * RB;
+  constexpr int kC32Sci = c32_sci<CIN>();           // input channels per weight stage
+  constexpr int kC32Ring = BB_CONV32_RING;
   constexpr int NCB = CIN / kC32Sci;                // weight stages per tap
   constexpr int NS = 9 * NCB;                       // stages
-  constexpr int WROW = kC32Sci * 4;                 // 128-byte weight rows (8 chunks)
+  constexpr int WROW = kC32Sci * 4;                 // 128- or 256-byte weight rows
+  constexpr int WCH = kC32Sci / 4;                  // 16-byte chunks per weight row
   constexpr int WBYTES = COUT * WROW;
   constexpr int NW = kC32Threads / 64;
   constexpr int GPW = WBYTES / 1024 / NW;           // 1-KB weight copies per wave per stage
@@ -95,22 +121,23 @@ __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __
   for (int k = wid; k < kC32Rows * NCH / 64; k += NW) {
     const int e = k * 64 + lane, r = e / NCH, lc = (e % NCH) ^ (r & 15);
     const int b = min(b0 + (r >> 6), nb - 1);  // boards past the batch read the last one (never stored)
-    c32_glds16(x + (size_t(b) * 64 + (r & 63)) * CIN + lc * 4, xs + k * 1024);
+    c32_glds16_async(x + (size_t(b) * 64 + (r & 63)) * CIN + lc * 4, xs + k * 1024);
   }
-  auto stage_w = [&](int st) {  // stage st: tap st / NCB, channels 32 (st % NCB) ... -> slot st % 2
+  auto stage_w = [&](int st) {  // stage st: tap st / NCB, channels SCI (st % NCB) ... -> slot st % RING
     uint8_t* wb = sm + XBYTES + (st % kC32Ring) * WBYTES;
     const float* ws = w + (size_t)(st / NCB) * COUT * CIN + (st % NCB) * kC32Sci;
 #pragma unroll
     for (int kq = 0; kq < GPW; ++kq) {
       const int k = wid + kq * NW;
-      const int e = k * 64 + lane, r = e / 8, lc = (e % 8) ^ ((r >> 1) & 7);
-      c32_glds16(ws + r * CIN + lc * 4, wb + k * 1024);
+      const int e = k * 64 + lane, r = e / WCH, lc = (e % WCH) ^ c32_wkey<kC32Sci>(r);
+      c32_glds16_async(ws + r * CIN + lc * 4, wb + k * 1024);
     }
   };
-  stage_w(0);
+#pragma unroll
+  for (int st = 0; st < kC32Ring - 1; ++st) stage_w(st);
   for (int i = tid; i < kC32Zero * NCH; i += kC32Threads)
     *reinterpret_cast<uint4*>(xs + kC32Rows * RB + i * 16) = make_uint4(0, 0, 0, 0);
-  __builtin_amdgcn_s_waitcnt(0);
+  C32_WAIT_VM_LGKM0((kC32Ring - 2) * GPW);  // the input tile and stage 0 (this wave's copies)
   __syncthreads();
 
   const int co0 = (wid % WN) * 64;
@@ -131,7 +158,8 @@ __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __
   int brow[TM];
 
   for (int st = 0; st < NS; ++st) {
-    if (st + 1 < NS) stage_w(st + 1);  // its slot was last read in stage st - 1, before that stage's barrier
+    // its slot was last read in stage st - 1, before that stage's barrier
+    if (st + kC32Ring - 1 < NS) stage_w(st + kC32Ring - 1);
     const int cb = st % NCB;
     if (cb == 0) {
       const int t = st / NCB, dy = t / 3 - 1, dx = t % 3 - 1;
@@ -150,12 +178,12 @@ __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int co = co0 + 16 * j + r16;
-        af[kb][j] = *reinterpret_cast<const f32x4*>(wb + abase[j] + (((4 * kb + g) ^ ((co >> 1) & 7)) << 4));
+        af[kb][j] = *reinterpret_cast<const f32x4*>(wb + abase[j] + (((4 * kb + g) ^ c32_wkey<kC32Sci>(co)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = brow[i];
-        bf[kb][i] = *reinterpret_cast<const f32x4*>(xs + row * RB + (((cb * 8 + 4 * kb + g) ^ (row & 15)) << 4));
+        bf[kb][i] = *reinterpret_cast<const f32x4*>(xs + row * RB + (((cb * WCH + 4 * kb + g) ^ (row & 15)) << 4));
       }
     }
 #pragma unroll
@@ -181,7 +209,13 @@ __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __
 #pragma unroll
           for (int e = 0; e < 4; ++e) dacc[j][i][e] += (double)acc[j][i][e];
     }
-    __builtin_amdgcn_s_waitcnt(0);  // the next stage's weights (this wave's copies; the barrier covers the rest)
+    // the next stage's weights (this wave's copies; the barrier covers the rest): every copy but the stages issued
+    // after it
+    {
+      const int after = min(NS, st + kC32Ring) - (st + 2);
+      if (after >= 1 && kC32Ring >= 3) C32_WAIT_VM_LGKM0(GPW);
+      else C32_WAIT_VM_LGKM0(0);
+    }
     __syncthreads();
   }
   // D[co0 + 16 j + 4 g + e][px0 + 16 i + r16]: 4 consecutive channels of one pixel = one 16-byte store

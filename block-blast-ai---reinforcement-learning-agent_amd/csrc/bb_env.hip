@@ -903,7 +903,10 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
 #define BB_ASYNC_SLEEP 1  // s_sleep of an idle search wave between polls
 #endif
 #ifndef BB_ASYNC_LINEONLY
-#define BB_ASYNC_LINEONLY 0  // search waves: slow_phase_wave's line-only second order (BB_SLOW_LINE_MIN tasks up)
+// search waves: slow_phase_wave's line-only second order above BB_SLOW_LINE_MIN tasks.  Round 3 measured it -1 to
+// -4% (short exact phases); on the quota schedule the exact phase is ~29% of a call and it measured +0.4%
+// (1.397e10 vs 1.392e10, three interleaved repeats; threshold 128: -2.8%; profiles/r05/ab/r05ab2_*)
+#define BB_ASYNC_LINEONLY 1
 #endif
 #ifndef BB_SEARCH_QUOTA
 // search waves: the quota pass schedule (gen_hands_quota, bb_solver.h); 0: gen_hands_multi's packed passes

@@ -52,6 +52,10 @@ VARIANTS = {
     "alo0": ["-DBB_ASYNC_LINEONLY=1", "-DBB_SLOW_LINE_MIN=0"],
     "alo128": ["-DBB_ASYNC_LINEONLY=1", "-DBB_SLOW_LINE_MIN=128"],
     "alo512": ["-DBB_ASYNC_LINEONLY=1"],
+    "aloff": ["-DBB_ASYNC_LINEONLY=0"],
+    # fp32 board convolutions (csrc/bb_conv32.hip): input channels per weight stage, LDS ring slots
+    "c32s64": ["-DBB_CONV32_SCI=64"],
+    "c32r3": ["-DBB_CONV32_RING=3"],
     "asw8": ["-DBB_ASYNC_SW=8"],
     # per-wave counters of rollout_async_kernel (tools/diag_async.py)
     "adiag": ["-DBB_ASYNC_DIAG=1"],
