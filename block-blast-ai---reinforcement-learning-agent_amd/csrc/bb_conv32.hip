@@ -42,10 +42,12 @@ constexpr int kC32Boards = 2;
 constexpr int kC32Rows = kC32Boards * 64;
 constexpr int kC32Zero = 16;
 #ifndef BB_CONV32_SCI
-#define BB_CONV32_SCI 32  // input channels per weight stage of the 128-input-channel layers (32 or 64)
+// input channels per weight stage of the 128-input-channel layers (32 or 64): 64 measured 103.9 vs 99.0 TFLOP/s on
+// conv 128 -> 128 at 65,536 boards (tools/bench_conv32.py, profiles/r05/conv32/)
+#define BB_CONV32_SCI 64
 #endif
 #ifndef BB_CONV32_RING
-#define BB_CONV32_RING 2  // weight-stage LDS ring slots (stages copied RING - 1 ahead)
+#define BB_CONV32_RING 2  // weight-stage LDS ring slots (stages copied RING - 1 ahead); 3: 103.3 TFLOP/s at SCI 32
 #endif
 #ifndef BB_CONV32_BLOCK
 #define BB_CONV32_BLOCK 16  // channels per fp32 MFMA chain before the fp64 add (16 or 32)
