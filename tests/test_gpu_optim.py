@@ -354,3 +354,43 @@ def test_conv3x3_forward_add(cuda):
     lib = K.L.load()
     assert lib.bb_conv3x3_forward_add(K._p(x), K._p(wf), n, 128, 128, K._p(a), K._p(y1), K._s(cuda)) == 0
     assert torch.equal(y1.view(torch.int16), (y0 + a).view(torch.int16))
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_deferred_wgrad_equals_inline(cuda, monkeypatch, graphs):
+    """The opt-in side-stream weight gradients (runtime.kernels.deferred_wgrad, BB_ASYNC_WGRAD=1): the bf16
+    optimizer step with the board convolutions' weight gradients on a side stream, joined before clip + Adam,
+    eager and graph-captured, equals the step with them inline (the same kernels and values; the weights after three
+    steps agree up to the run-to-run rounding of MIOpen's first-layer weight gradient, which uses atomics)."""
+    import runtime.kernels as K
+    from agents import PPOAgent, PPOConfig
+
+    g = torch.Generator().manual_seed(3)
+    b = 512
+    x = (torch.rand(b, 4, 8, 8, generator=g) < 0.4).float().to(cuda)
+    mask = (torch.rand(b, 192, generator=g) < 0.3).float()
+    mask[:, 0] = 1.0
+    act = torch.multinomial(mask, 1, generator=g).squeeze(1).to(cuda)
+    mask = mask.to(cuda)
+    old = (-3.0 * torch.rand(b, generator=g)).to(cuda)
+    adv, ret = torch.randn(b, generator=g).to(cuda), torch.randn(b, generator=g).to(cuda)
+    res = {}
+    for on in (False, True):
+        monkeypatch.setattr(K, "ASYNC_WGRAD", on)
+        torch.manual_seed(0)
+        agent = PPOAgent(PPOConfig(batch_size=b), device=cuda, sample_seed=1)
+        agent.autocast_dtype = torch.bfloat16
+        agent.use_graphs = graphs
+        agent.train()
+        for m in agent.network.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+        for _ in range(3):
+            agent.train_minibatch(x, mask, act, old, adv, ret)
+        torch.cuda.synchronize()
+        res[on] = {n: p.detach().clone() for n, p in agent.network.named_parameters()}
+    for n, p in res[True].items():
+        if n.startswith("conv_encoder.0."):
+            assert torch.allclose(p, res[False][n], rtol=1e-3, atol=1e-5), n
+        else:
+            assert torch.allclose(p, res[False][n], rtol=1e-4, atol=1e-6), n
