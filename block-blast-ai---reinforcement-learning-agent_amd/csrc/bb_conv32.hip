@@ -238,21 +238,32 @@ __global__ void __launch_bounds__(kC32Threads) conv32_fwd_kernel(const float* __
 // network.py:89-117: the first fc_encoder layer has K = 8,192, where hipBLASLt's fp32 order cost more than
 // north_star's 1e-5 at the logits after the batch-statistics BatchNorms, tools/diag_net_fp32.py).  Every
 // output is the fp64 sum of 16-product fp32 MFMA chains plus the bias, rounded once.  x [M][K], w [N][K]
-// row-major (K contiguous), y [M][N]; N % 128 == 0, K % 32 == 0.  Workgroup: 4 waves, 64 rows x 128 columns;
-// waves 2 (m) x 2 (n) of 32 x 64; stages of 32 k through a 2-slot LDS ring (direct global -> LDS copies),
+// row-major (K contiguous), y [M][N]; N % 128 == 0, K % 32 == 0.  Workgroup: BM (64 or 128) rows x 128 columns,
+// waves BM / 32 (m) x 2 (n) of 32 x 64; stages of 32 k through a 2-slot LDS ring (direct global -> LDS copies),
 // rows of 128 bytes XOR-swizzled by chunk ^ ((row >> 1) & 7).
 // ---------------------------------------------------------------------------
-constexpr int kL32Threads = 256;
-constexpr int kL32BM = 64, kL32BN = 128, kL32BK = 32;
+// Two tile heights: 128 rows (8 waves; each W stage serves twice the rows, registers capped for two
+// workgroups per CU, 12 VGPRs spilled) when the grid still has >= BB_LINEAR32_BIG workgroups, else 64 rows (4 waves) so that
+// small batches spread over more CUs.  Microbench (tools/bench_conv32.py, 8192 -> 512): 65,536 rows
+// 7.97 -> 5.42 ms with the taller tile; 2,048 rows 0.42 ms (64) vs 0.75 ms (128).
+#ifndef BB_LINEAR32_BIG
+#define BB_LINEAR32_BIG 1024
+#endif
+constexpr int kL32BN = 128, kL32BK = 32;
+template <int BM>
+constexpr int l32_threads() { return 64 * (BM / 32) * 2; }  // waves: BM / 32 (m) x 2 (n), each 32 m x 64 n
 
-__global__ void __launch_bounds__(kL32Threads) linear32_kernel(const float* __restrict__ x,
-                                                               const float* __restrict__ w,
-                                                               const float* __restrict__ bias,
-                                                               float* __restrict__ y, int M, int N, int K) {
+template <int BM>
+__global__ void __launch_bounds__(l32_threads<BM>()) __attribute__((amdgpu_waves_per_eu(BM == 128 ? 4 : 1)))
+linear32_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                float* __restrict__ y, int M, int N, int K) {
+  constexpr int kL32BM = BM, kL32Threads = l32_threads<BM>();
   constexpr int ABYTES = kL32BM * kL32BK * 4, BBYTES = kL32BN * kL32BK * 4;
   constexpr int SBYTES = ABYTES + BBYTES;
   constexpr int NW = kL32Threads / 64;
   constexpr int TM = 2, TN = 4;  // 16 x 16 tiles per wave: 32 m x 64 n
+  constexpr int GA = ABYTES / 1024 / NW, GB = BBYTES / 1024 / NW;  // 1-KB copies per wave per stage
+  static_assert(GA >= 1 && GB >= 1, "stage smaller than one copy per wave");
   __shared__ __attribute__((aligned(16))) uint8_t sm[2 * SBYTES];
   const int tid = threadIdx.x;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -264,21 +275,21 @@ __global__ void __launch_bounds__(kL32Threads) linear32_kernel(const float* __re
     uint8_t* b = a + ABYTES;
     const int k0 = st * kL32BK;
 #pragma unroll
-    for (int kq = 0; kq < ABYTES / 1024 / NW; ++kq) {
+    for (int kq = 0; kq < GA; ++kq) {
       const int kk = wid + kq * NW, e = kk * 64 + lane, r = e / 8, lc = (e % 8) ^ ((r >> 1) & 7);
       const int row = min(m0 + r, M - 1);  // rows past M read the last one (never stored)
-      c32_glds16(x + (size_t)row * K + k0 + lc * 4, a + kk * 1024);
+      c32_glds16_async(x + (size_t)row * K + k0 + lc * 4, a + kk * 1024);
     }
 #pragma unroll
-    for (int kq = 0; kq < BBYTES / 1024 / NW; ++kq) {
+    for (int kq = 0; kq < GB; ++kq) {
       const int kk = wid + kq * NW, e = kk * 64 + lane, r = e / 8, lc = (e % 8) ^ ((r >> 1) & 7);
-      c32_glds16(w + (size_t)(n0 + r) * K + k0 + lc * 4, b + kk * 1024);
+      c32_glds16_async(w + (size_t)(n0 + r) * K + k0 + lc * 4, b + kk * 1024);
     }
   };
   stage(0);
-  __builtin_amdgcn_s_waitcnt(0);
+  C32_WAIT_VM_LGKM0(0);
   __syncthreads();
-  const int wm = (wid & 1) * 32, wn = (wid >> 1) * 64;
+  const int wm = (wid % (kL32BM / 32)) * 32, wn = (wid / (kL32BM / 32)) * 64;
   double dacc[TN][TM][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j)
@@ -322,7 +333,7 @@ __global__ void __launch_bounds__(kL32Threads) linear32_kernel(const float* __re
 #pragma unroll
           for (int e = 0; e < 4; ++e) dacc[j][i][e] += (double)acc[j][i][e];
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    C32_WAIT_VM_LGKM0(0);  // the next stage (this wave's copies; the barrier covers the rest)
     __syncthreads();
   }
   // D[n = wn + 16 j + 4 g + e][m = wm + 16 i + r16]: 4 consecutive outputs of one row = one 16-byte store
@@ -371,8 +382,12 @@ hipError_t launch_conv3x3_f32_forward(const float* x, const float* w, int nb, in
 hipError_t launch_linear_f32(const float* x, const float* w, const float* bias, int M, int N, int K, float* y,
                              hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || N % kL32BN || K % kL32BK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(linear32_kernel, dim3((M + kL32BM - 1) / kL32BM, N / kL32BN), dim3(kL32Threads), 0, s, x, w,
-                     bias, y, M, N, K);
+  if ((long)((M + 127) / 128) * (N / kL32BN) >= BB_LINEAR32_BIG)
+    hipLaunchKernelGGL(linear32_kernel<128>, dim3((M + 127) / 128, N / kL32BN), dim3(l32_threads<128>()), 0, s, x,
+                       w, bias, y, M, N, K);
+  else
+    hipLaunchKernelGGL(linear32_kernel<64>, dim3((M + 63) / 64, N / kL32BN), dim3(l32_threads<64>()), 0, s, x, w,
+                       bias, y, M, N, K);
   return hipGetLastError();
 }
 

@@ -132,7 +132,9 @@ def test_conv32_function_autograd(cuda):
         assert rel < 1e-5, rel
 
 
-@pytest.mark.parametrize("m,n,k", [(1, 128, 32), (77, 512, 8192), (2048, 512, 8192), (300, 256, 512), (64, 128, 256)])
+# the last two take the 128-row tile (>= 1,024 workgroups), ragged in M
+@pytest.mark.parametrize("m,n,k", [(1, 128, 32), (77, 512, 8192), (2048, 512, 8192), (300, 256, 512), (64, 128, 256),
+                                   (32700, 512, 512), (16385, 1024, 256)])
 def test_linear_f32_within_error_bound(cuda, m, n, k):
     """bb_linear_f32 (nn.Linear forward) against float64: |y - y64| <= 2^-24 |y64| + gamma_16 sum|x w| (+ the
     bias, added in fp64 before the one rounding); ragged M; its RMS error not above hipBLASLt's fp32 at K >= 512."""

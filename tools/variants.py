@@ -56,6 +56,8 @@ VARIANTS = {
     # fp32 board convolutions (csrc/bb_conv32.hip): input channels per weight stage, LDS ring slots
     "c32s64": ["-DBB_CONV32_SCI=64"],
     "c32r3": ["-DBB_CONV32_RING=3"],
+    "l32bm64": ["-DBB_LINEAR32_BM=64", "-DBB_LINEAR32_WPE=1"],
+    "l32wpe1": ["-DBB_LINEAR32_WPE=1"],
     "asw8": ["-DBB_ASYNC_SW=8"],
     # per-wave counters of rollout_async_kernel (tools/diag_async.py)
     "adiag": ["-DBB_ASYNC_DIAG=1"],
