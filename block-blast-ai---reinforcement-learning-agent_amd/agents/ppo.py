@@ -529,6 +529,9 @@ class PPOAgent(BaseAgent):
         return split
 
     def _minibatch_loss(self, x, masks, actions, old_log_probs, advantages, returns):
+        """(loss, stats) of one minibatch.  In the segmented data-parallel mode the forward is cut at the conv
+        stack's output (self._seg): that loss must go through _optimizer_step, whose backward runs both
+        segments; a bare loss.backward() would stop at the cut."""
         cfg = self.config
         if self._segmented():
             self.network.grad_split = []

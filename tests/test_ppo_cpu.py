@@ -114,6 +114,7 @@ def _ddp_worker(rank, world, port, q):
 
     torch.manual_seed(100 + rank)  # different init per rank -> broadcast must fix it
     agent = PPOAgent(PPOConfig(), device=torch.device("cpu"), sample_seed=0)
+    agent.dp_overlap = "graph-split"  # one backward over the whole graph (the segmented loss needs _optimizer_step)
     agent.network.eval()
     broadcast_parameters(agent)
     g = torch.Generator().manual_seed(rank)
