@@ -178,9 +178,12 @@ def load_traffic(n_envs: int, mode: str, steps_per_launch: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20,
+    # 200 timed launches after 20 warm-up launches (0.13 s of kernels): the first launches after the reset run the
+    # young-episode mix and read ~3.5% under the steady state of a PPO run (20 after 5: 1.337e10; 20 after 100:
+    # 1.380e10; 200 after 20 or 100: 1.390e10; 1,280 after 128: 1.391e10, profiles/r05/r05wu_*)
+    ap.add_argument("--steps", type=int, default=200,
                     help="timed bench steps: bb_rollout launches of T env-steps (rollout) or bb_step launches (step)")
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
