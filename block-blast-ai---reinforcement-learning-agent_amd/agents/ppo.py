@@ -312,6 +312,7 @@ class PPOAgent(BaseAgent):
         self.dp_bucket_floats = 1 << 21
         self.dp_overlap = "graph-segments"
         self._seg = None  # (conv-stack output, its detached leaf) of the last segmented forward
+        self._loss_seed: Optional[torch.Tensor] = None  # _backward_loss
         self._dp_hooks = None
         self._dp_hooks_on = True  # off while a graph without collectives is captured
         self._dp_works: List[Any] = []
@@ -355,13 +356,15 @@ class PPOAgent(BaseAgent):
         self._flat_grad = None  # gradient views must follow the parameters' strides
         self._remove_dp_hooks()
 
-    def _raw(self, x: torch.Tensor):
+    def _raw(self, x: torch.Tensor, keep_dtype: bool = False):
+        """(logits, value) of the network; under autocast cast to f32 unless keep_dtype (the fused loss reads
+        the bf16 outputs as they are: bb_ppo_loss_forward_bf16)."""
         if self.channels_last and x.is_cuda:
             x = x.contiguous(memory_format=torch.channels_last)
         if self.autocast_dtype is not None and x.is_cuda:
             with torch.autocast("cuda", dtype=self.autocast_dtype, cache_enabled=False):
                 logits, value = self.network.raw(x)
-            return logits.float(), value.float()
+            return (logits, value) if keep_dtype else (logits.float(), value.float())
         return self.network.raw(x)
 
     def _obs_to_device(self, obs: Dict[str, Any]):
@@ -533,19 +536,28 @@ class PPOAgent(BaseAgent):
         stack's output (self._seg): that loss must go through _optimizer_step, whose backward runs both
         segments; a bare loss.backward() would stop at the cut."""
         cfg = self.config
+        keep = self.fused_loss and x.is_cuda
         if self._segmented():
             self.network.grad_split = []
             try:
-                logits, values = self._raw(x)
+                logits, values = self._raw(x, keep)
             finally:
                 cut, self.network.grad_split = self.network.grad_split, None
             self._seg = cut[0] if len(cut) == 1 else None
         else:
-            logits, values = self._raw(x)
+            logits, values = self._raw(x, keep)
         if self.fused_loss and logits.is_cuda:  # bb_ppo_loss_forward/backward
             return K.PPOLossFunction.apply(logits, values, masks, actions, old_log_probs, advantages, returns,
                                            cfg.clip_epsilon, cfg.value_coef, cfg.entropy_coef)
         return ppo_loss_torch(logits, values, masks, actions, old_log_probs, advantages, returns, cfg)
+
+    def _backward_loss(self, loss: torch.Tensor) -> None:
+        """loss.backward() seeded with a persistent 1.0 (loss.backward() fills a fresh one: one more kernel in every
+        graph replay).  The seed is made by the first (eager) step, before any capture."""
+        seed = self._loss_seed
+        if seed is None or seed.device != loss.device or seed.dtype != loss.dtype:
+            seed = self._loss_seed = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(seed)
 
     def _backward_segments(self, loss: torch.Tensor, world: int) -> None:
         """Segmented data-parallel backward: heads + FC, their bucket's all-reduce issued (async), the conv
@@ -555,7 +567,7 @@ class PPOAgent(BaseAgent):
         h, hd = self._seg
         self._seg = None
         flat.zero_()
-        loss.backward()
+        self._backward_loss(loss)
         w_fc = dist.all_reduce(flat[split:], async_op=True)
         with K.deferred_wgrad(self.device):  # joined before the conv bucket's all-reduce
             h.backward(hd.grad)
@@ -573,7 +585,7 @@ class PPOAgent(BaseAgent):
             flat = self._grad_buffer()
             flat.zero_()
             self._dp_arm()
-            loss.backward()
+            self._backward_loss(loss)
             self._dp_finish(world)
         else:  # autograd hands its gradient tensors over: no zero fill, no accumulating adds
             self._flat_grad = None
@@ -581,7 +593,7 @@ class PPOAgent(BaseAgent):
             for p in self.network.parameters():
                 p.grad = None
             with K.deferred_wgrad(self.device):  # conv weight gradients beside the rest of the backward
-                loss.backward()
+                self._backward_loss(loss)
         self._clip_and_step()
 
     def _fused_clip_adam(self) -> bool:
@@ -716,7 +728,7 @@ class PPOAgent(BaseAgent):
             with torch.cuda.graph(graphs[0], stream=side):  # A1: zero, forward, loss, heads + FC backward
                 flat.zero_()
                 loss, stats = self._minibatch_loss(*static_in)
-                loss.backward()
+                self._backward_loss(loss)
                 del loss
             h, hd = self._seg
             self._seg = None
@@ -744,7 +756,7 @@ class PPOAgent(BaseAgent):
                     flat.zero_()
                     loss, stats = self._minibatch_loss(*static_in)
                     with K.deferred_wgrad(self.device):
-                        loss.backward()
+                        self._backward_loss(loss)
                     del loss
             finally:
                 self._dp_hooks_on = True

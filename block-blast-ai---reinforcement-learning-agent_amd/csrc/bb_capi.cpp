@@ -709,31 +709,67 @@ extern "C" int64_t bb_ppo_loss_workspace_bytes(int32_t B) {
   return ppo_loss_workspace_bytes(B);
 }
 
+namespace {
+int loss_forward_impl(const void* d_logits, const void* d_values, int bf16, const float* d_mask,
+                      const int64_t* d_actions, const float* d_old_logp, const float* d_adv, const float* d_ret,
+                      int32_t B, float clip, float value_coef, float entropy_coef, double* d_ws, float* d_stats,
+                      float* d_loss, void* stream, const char* what) {
+  if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret || !d_ws ||
+      !d_stats)
+    return fail(nullptr, BB_ERR_ARG, std::string(what) + ": bad arguments");
+  hipError_t st = launch_ppo_loss_forward(d_logits, d_values, bf16, d_mask, d_actions, d_old_logp, d_adv, d_ret, B,
+                                          clip, value_coef, entropy_coef, d_ws, d_stats, d_loss, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, what);
+  return BB_OK;
+}
+
+int loss_backward_impl(const void* d_logits, const void* d_values, int bf16, const float* d_mask,
+                       const int64_t* d_actions, const float* d_old_logp, const float* d_adv, const float* d_ret,
+                       int32_t B, float clip, float value_coef, float entropy_coef, const float* d_grad_loss,
+                       void* d_dlogits, void* d_dvalues, void* stream, const char* what) {
+  if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret ||
+      !d_grad_loss || !d_dlogits || !d_dvalues)
+    return fail(nullptr, BB_ERR_ARG, std::string(what) + ": bad arguments");
+  hipError_t st = launch_ppo_loss_backward(d_logits, d_values, bf16, d_mask, d_actions, d_old_logp, d_adv, d_ret, B,
+                                           clip, value_coef, entropy_coef, d_grad_loss, d_dlogits, d_dvalues,
+                                           (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, what);
+  return BB_OK;
+}
+}  // namespace
+
 extern "C" int bb_ppo_loss_forward(const float* d_logits, const float* d_values, const float* d_mask,
                                    const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
                                    const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
                                    double* d_ws, float* d_stats, float* d_loss, void* stream) {
-  if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret || !d_ws ||
-      !d_stats)
-    return fail(nullptr, BB_ERR_ARG, "bb_ppo_loss_forward: bad arguments");
-  hipError_t st = launch_ppo_loss_forward(d_logits, d_values, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip,
-                                          value_coef, entropy_coef, d_ws, d_stats, d_loss, (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_ppo_loss_forward");
-  return BB_OK;
+  return loss_forward_impl(d_logits, d_values, 0, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip, value_coef,
+                           entropy_coef, d_ws, d_stats, d_loss, stream, "bb_ppo_loss_forward");
 }
 
 extern "C" int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const float* d_mask,
                                     const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
                                     const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
                                     const float* d_grad_loss, float* d_dlogits, float* d_dvalues, void* stream) {
-  if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret ||
-      !d_grad_loss || !d_dlogits || !d_dvalues)
-    return fail(nullptr, BB_ERR_ARG, "bb_ppo_loss_backward: bad arguments");
-  hipError_t st = launch_ppo_loss_backward(d_logits, d_values, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip,
-                                           value_coef, entropy_coef, d_grad_loss, d_dlogits, d_dvalues,
-                                           (hipStream_t)stream);
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_ppo_loss_backward");
-  return BB_OK;
+  return loss_backward_impl(d_logits, d_values, 0, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip, value_coef,
+                            entropy_coef, d_grad_loss, d_dlogits, d_dvalues, stream, "bb_ppo_loss_backward");
+}
+
+extern "C" int bb_ppo_loss_forward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
+                                        const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                                        const float* d_ret, int32_t B, float clip, float value_coef,
+                                        float entropy_coef, double* d_ws, float* d_stats, float* d_loss,
+                                        void* stream) {
+  return loss_forward_impl(d_logits, d_values, 1, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip, value_coef,
+                           entropy_coef, d_ws, d_stats, d_loss, stream, "bb_ppo_loss_forward_bf16");
+}
+
+extern "C" int bb_ppo_loss_backward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
+                                         const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                                         const float* d_ret, int32_t B, float clip, float value_coef,
+                                         float entropy_coef, const float* d_grad_loss, void* d_dlogits,
+                                         void* d_dvalues, void* stream) {
+  return loss_backward_impl(d_logits, d_values, 1, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip, value_coef,
+                            entropy_coef, d_grad_loss, d_dlogits, d_dvalues, stream, "bb_ppo_loss_backward_bf16");
 }
 
 namespace {

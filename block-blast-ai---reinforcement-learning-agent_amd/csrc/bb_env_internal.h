@@ -129,13 +129,15 @@ hipError_t launch_linear_f32(const float* x, const float* w, const float* bias, 
                              hipStream_t s);
 
 int64_t ppo_loss_workspace_bytes(int B);
-hipError_t launch_ppo_loss_forward(const float* logits, const float* values, const float* mask, const int64_t* actions,
-                                   const float* old_logp, const float* adv, const float* ret, int B, float clip,
-                                   float vcoef, float ecoef, double* ws, float* stats, float* loss, hipStream_t s);
-hipError_t launch_ppo_loss_backward(const float* logits, const float* values, const float* mask,
+// logits / values (and backward's dlogits / dvalues): f32, or bf16 when bf16 != 0
+hipError_t launch_ppo_loss_forward(const void* logits, const void* values, int bf16, const float* mask,
+                                   const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
+                                   int B, float clip, float vcoef, float ecoef, double* ws, float* stats, float* loss,
+                                   hipStream_t s);
+hipError_t launch_ppo_loss_backward(const void* logits, const void* values, int bf16, const float* mask,
                                     const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
-                                    int B, float clip, float vcoef, float ecoef, const float* gloss, float* dlogits,
-                                    float* dvalues, hipStream_t s);
+                                    int B, float clip, float vcoef, float ecoef, const float* gloss, void* dlogits,
+                                    void* dvalues, hipStream_t s);
 
 constexpr int kOptMaxTensors = 48;  // == BB_OPT_MAX_TENSORS
 int64_t adam_clip_workspace_bytes(int count, const int64_t* n);

@@ -19,8 +19,12 @@
 // clip_fraction = mean(|r - 1| > c)) come from fp64 block partials summed in a
 // fixed order.  Backward follows torch's autograd rules: torch.min splits ties
 // half/half, clamp passes the gradient on its closed interval, log divides by
-// the clamped value.
+// the clamped value.  Logits and values may be bf16 (the autocast network's
+// outputs): widened exactly on load, and their gradients rounded to bf16 (to
+// nearest even) on store -- the values of autograd's casts around an fp32 loss,
+// without the four cast kernels.
 #include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
 #include <math.h>
 
 #include "bb_env_internal.h"
@@ -57,12 +61,29 @@ struct RowFwd {
   float logp, ent;
 };
 
-__device__ __forceinline__ void row_forward(const float* __restrict__ logits, const float* __restrict__ mask,
+// logits / values / their gradients: f32, or bf16 (BF)
+template <bool BF>
+__device__ __forceinline__ float ldv(const void* __restrict__ p, int64_t i) {
+  if constexpr (BF) return __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(p)[i] << 16);
+  return reinterpret_cast<const float*>(p)[i];
+}
+template <bool BF>
+__device__ __forceinline__ void stv(void* __restrict__ p, int64_t i, float v) {
+  if constexpr (BF) {
+    const __hip_bfloat16 b = __float2bfloat16(v);  // round to nearest even, as torch's cast
+    reinterpret_cast<uint16_t*>(p)[i] = *reinterpret_cast<const uint16_t*>(&b);
+  } else {
+    reinterpret_cast<float*>(p)[i] = v;
+  }
+}
+
+template <bool BF>
+__device__ __forceinline__ void row_forward(const void* __restrict__ logits, const float* __restrict__ mask,
                                             int64_t row, int64_t a, int lane, RowFwd& r) {
   float x[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    x[j] = logits[row * 192 + j * 64 + lane];
+    x[j] = ldv<BF>(logits, row * 192 + j * 64 + lane);
     r.valid[j] = mask[row * 192 + j * 64 + lane] != 0.f;
   }
   float mx = -INFINITY;
@@ -101,8 +122,9 @@ __device__ __forceinline__ void row_forward(const float* __restrict__ logits, co
   r.ent = -wsum(h);
 }
 
+template <bool BF>
 __global__ void __launch_bounds__(kLossThreads) ppo_loss_fwd_kernel(
-    const float* __restrict__ logits, const float* __restrict__ values, const float* __restrict__ mask,
+    const void* __restrict__ logits, const void* __restrict__ values, const float* __restrict__ mask,
     const int64_t* __restrict__ actions, const float* __restrict__ old_logp, const float* __restrict__ adv,
     const float* __restrict__ ret, int B, float clip, double* __restrict__ part) {
   __shared__ double red[kStats][kRowsPerBlock];
@@ -110,11 +132,11 @@ __global__ void __launch_bounds__(kLossThreads) ppo_loss_fwd_kernel(
   double acc[kStats] = {0.0, 0.0, 0.0, 0.0, 0.0};
   for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < B; row += (int64_t)gridDim.x * kRowsPerBlock) {
     RowFwd r;
-    row_forward(logits, mask, row, actions[row], lane, r);
+    row_forward<BF>(logits, mask, row, actions[row], lane, r);
     const float A = adv[row];
     const float ratio = expf(__fsub_rn(r.logp, old_logp[row]));
     const float s1 = __fmul_rn(ratio, A), s2 = __fmul_rn(fminf(fmaxf(ratio, 1.f - clip), 1.f + clip), A);
-    const float dv = __fsub_rn(values[row], ret[row]);
+    const float dv = __fsub_rn(ldv<BF>(values, row), ret[row]);
     const float rm1 = __fsub_rn(ratio, 1.f);
     acc[0] += (double)(-fminf(s1, s2));
     acc[1] += (double)__fmul_rn(dv, dv);
@@ -160,18 +182,19 @@ __global__ void ppo_loss_finalize_kernel(const double* __restrict__ part, int nb
   }
 }
 
+template <bool BF>
 __global__ void __launch_bounds__(kLossThreads) ppo_loss_bwd_kernel(
-    const float* __restrict__ logits, const float* __restrict__ values, const float* __restrict__ mask,
+    const void* __restrict__ logits, const void* __restrict__ values, const float* __restrict__ mask,
     const int64_t* __restrict__ actions, const float* __restrict__ old_logp, const float* __restrict__ adv,
     const float* __restrict__ ret, int B, float clip, float vcoef, float ecoef, const float* __restrict__ gloss,
-    float* __restrict__ dlogits, float* __restrict__ dvalues) {
+    void* __restrict__ dlogits, void* __restrict__ dvalues) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float g = gloss[0];
   const float invB = 1.f / (float)B;
   for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < B; row += (int64_t)gridDim.x * kRowsPerBlock) {
     const int64_t a = actions[row];
     RowFwd r;
-    row_forward(logits, mask, row, a, lane, r);
+    row_forward<BF>(logits, mask, row, a, lane, r);
     const float A = adv[row];
     const float ratio = expf(__fsub_rn(r.logp, old_logp[row]));
     const float s1 = __fmul_rn(ratio, A), s2 = __fmul_rn(fminf(fmaxf(ratio, 1.f - clip), 1.f + clip), A);
@@ -181,7 +204,7 @@ __global__ void __launch_bounds__(kLossThreads) ppo_loss_bwd_kernel(
     const float g2 = s2 < s1 ? gmin : (s2 > s1 ? 0.f : 0.5f * gmin);
     const bool in_clip = ratio >= 1.f - clip && ratio <= 1.f + clip;
     const float glogp = (g1 * A + (in_clip ? g2 * A : 0.f)) * ratio;  // d exp(x)/dx = exp(x)
-    if (lane == 0) dvalues[row] = vcoef * g * invB * 2.f * __fsub_rn(values[row], ret[row]);  // mse_loss
+    if (lane == 0) stv<BF>(dvalues, row, vcoef * g * invB * 2.f * __fsub_rn(ldv<BF>(values, row), ret[row]));  // mse
     const float gent = -ecoef * g * invB;  // ecoef * (-mean(ent))
     // log(clamp(P_a, eps, 1 - eps)): passes where eps <= P_a <= 1 - eps, divided by the clamped value
     const float gPa = (r.pa >= kEps32 && r.pa <= 1.f - kEps32) ? glogp / r.pa : 0.f;
@@ -210,7 +233,7 @@ __global__ void __launch_bounds__(kLossThreads) ppo_loss_bwd_kernel(
     dot = wsum(dot);
     // softmax backward: dz_k = p_k (gp_k - sum_j gp_j p_j); masked entries have p = 0
 #pragma unroll
-    for (int j = 0; j < 3; ++j) dlogits[row * 192 + j * 64 + lane] = r.p[j] * (gp[j] - dot);
+    for (int j = 0; j < 3; ++j) stv<BF>(dlogits, row * 192 + j * 64 + lane, r.p[j] * (gp[j] - dot));
   }
 }
 
@@ -223,22 +246,31 @@ int loss_blocks(int B) {
 
 int64_t ppo_loss_workspace_bytes(int B) { return (int64_t)sizeof(double) * kStats * loss_blocks(B); }
 
-hipError_t launch_ppo_loss_forward(const float* logits, const float* values, const float* mask, const int64_t* actions,
-                                   const float* old_logp, const float* adv, const float* ret, int B, float clip,
-                                   float vcoef, float ecoef, double* ws, float* stats, float* loss, hipStream_t s) {
+hipError_t launch_ppo_loss_forward(const void* logits, const void* values, int bf16, const float* mask,
+                                   const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
+                                   int B, float clip, float vcoef, float ecoef, double* ws, float* stats, float* loss,
+                                   hipStream_t s) {
   const int nb = loss_blocks(B);
-  hipLaunchKernelGGL(ppo_loss_fwd_kernel, dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask, actions, old_logp,
-                     adv, ret, B, clip, ws);
+  if (bf16)
+    hipLaunchKernelGGL(ppo_loss_fwd_kernel<true>, dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask, actions,
+                       old_logp, adv, ret, B, clip, ws);
+  else
+    hipLaunchKernelGGL(ppo_loss_fwd_kernel<false>, dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask, actions,
+                       old_logp, adv, ret, B, clip, ws);
   hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(64), 0, s, ws, nb, B, vcoef, ecoef, stats, loss);
   return hipGetLastError();
 }
 
-hipError_t launch_ppo_loss_backward(const float* logits, const float* values, const float* mask,
+hipError_t launch_ppo_loss_backward(const void* logits, const void* values, int bf16, const float* mask,
                                     const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
-                                    int B, float clip, float vcoef, float ecoef, const float* gloss, float* dlogits,
-                                    float* dvalues, hipStream_t s) {
-  hipLaunchKernelGGL(ppo_loss_bwd_kernel, dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits, values, mask,
-                     actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues);
+                                    int B, float clip, float vcoef, float ecoef, const float* gloss, void* dlogits,
+                                    void* dvalues, hipStream_t s) {
+  if (bf16)
+    hipLaunchKernelGGL(ppo_loss_bwd_kernel<true>, dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits, values, mask,
+                       actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues);
+  else
+    hipLaunchKernelGGL(ppo_loss_bwd_kernel<false>, dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits, values,
+                       mask, actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues);
   return hipGetLastError();
 }
 

@@ -531,7 +531,11 @@ class PPOLossFunction(torch.autograd.Function):
     def forward(ctx, logits, values, masks, actions, old_log_probs, advantages, returns, clip: float,
                 value_coef: float, entropy_coef: float):
         _need_cuda(logits, values, masks, actions, old_log_probs, advantages, returns)
-        ins = (logits.contiguous().float(), values.contiguous().float(), masks.contiguous().float(),
+        # bf16 logits and values (the autocast network's) are read as they are and get bf16 gradients
+        # (bb_ppo_loss_*_bf16: the values of autograd's casts, without the cast launches)
+        bf16 = logits.dtype == torch.bfloat16 and values.dtype == torch.bfloat16
+        act = torch.bfloat16 if bf16 else torch.float32
+        ins = (logits.contiguous().to(act), values.contiguous().to(act), masks.contiguous().float(),
                actions.contiguous().long(), old_log_probs.contiguous().float(), advantages.contiguous().float(),
                returns.contiguous().float())
         b = ins[0].shape[0]
@@ -540,24 +544,29 @@ class PPOLossFunction(torch.autograd.Function):
         ws = torch.empty((lib.bb_ppo_loss_workspace_bytes(b) + 7) // 8, dtype=torch.float64, device=dev)
         stats = torch.empty(6, dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        L.check(lib.bb_ppo_loss_forward(*[_p(t) for t in ins], b, float(clip), float(value_coef),
-                                        float(entropy_coef), _p(ws), _p(stats), _p(loss), _s(dev)),
+        fn = lib.bb_ppo_loss_forward_bf16 if bf16 else lib.bb_ppo_loss_forward
+        L.check(fn(*[_p(t) for t in ins], b, float(clip), float(value_coef), float(entropy_coef), _p(ws), _p(stats),
+                   _p(loss), _s(dev)),
                 "bb_ppo_loss_forward")
         ctx.save_for_backward(*ins)
         ctx.coef = (float(clip), float(value_coef), float(entropy_coef))
+        ctx.bf16 = bf16
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics
         return loss, stats
 
     @staticmethod
     def backward(ctx, grad_loss, grad_stats):
         ins = ctx.saved_tensors
+        if grad_loss is None:
+            return (None,) * 10
         b = ins[0].shape[0]
         dev = ins[0].device
         g = grad_loss.float().reshape(1).contiguous()
         dlogits = torch.empty_like(ins[0])
         dvalues = torch.empty_like(ins[1])
-        L.check(L.load().bb_ppo_loss_backward(*[_p(t) for t in ins], b, *ctx.coef, _p(g), _p(dlogits), _p(dvalues),
-                                              _s(dev)),
+        fn = L.load().bb_ppo_loss_backward_bf16 if ctx.bf16 else L.load().bb_ppo_loss_backward
+        L.check(fn(*[_p(t) for t in ins], b, *ctx.coef, _p(g), _p(dlogits), _p(dvalues), _s(dev)),
                 "bb_ppo_loss_backward")
         return dlogits, dvalues, None, None, None, None, None, None, None, None
 

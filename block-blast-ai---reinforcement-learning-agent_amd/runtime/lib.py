@@ -60,7 +60,7 @@ class Info(C.Structure):
     ]
 
 
-ABI_VERSION = 6  # include/bbvec.h BB_ABI_VERSION
+ABI_VERSION = 7  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -160,6 +160,8 @@ SIGNATURES = {
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),
     "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
     "bb_ppo_loss_backward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
+    "bb_ppo_loss_forward_bf16": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
+    "bb_ppo_loss_backward_bf16": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
     "bb_adam_clip_workspace_bytes": (C.c_int64, [_I32, _P]),
     "bb_adam_clip_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double, _F,
                                     _P, _P, _P]),

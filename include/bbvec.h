@@ -32,11 +32,12 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 6  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
+#define BB_ABI_VERSION 7  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
                               4: bb_conv_in_* and bb_relu_bias_grad* removed;
                               5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed;
                               6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
-                                 bb_conv3x3_f32_prep / _forward, bb_linear_f32 */
+                                 bb_conv3x3_f32_prep / _forward, bb_linear_f32;
+                              7: bb_ppo_loss_forward_bf16 / _backward_bf16 */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -348,6 +349,17 @@ int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const flo
                          const float* d_ret, int32_t B, float clip, float value_coef,
                          float entropy_coef, const float* d_grad_loss, float* d_dlogits,
                          float* d_dvalues, void* stream);
+/* The same loss on bf16 logits [B][192] and values [B] (the autocast network's outputs), widened exactly on
+ * load; the backward writes d/dlogits and d/dvalues in bf16, rounded to nearest even: exactly the values of
+ * autograd's casts around the f32 loss (bit-identical), without the four cast launches. */
+int bb_ppo_loss_forward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
+                             const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                             const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
+                             double* d_ws, float* d_stats, float* d_loss, void* stream);
+int bb_ppo_loss_backward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
+                              const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                              const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
+                              const float* d_grad_loss, void* d_dlogits, void* d_dvalues, void* stream);
 
 /* The CNN's 3x3 / padding-1 convolutions over 8x8 boards (network.py:75-117,
  * ResidualBlock network.py:14-30; nn.Conv2d.forward and its autograd

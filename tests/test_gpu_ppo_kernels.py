@@ -281,3 +281,35 @@ def test_fused_ppo_loss_matches_torch(cuda, density):
     scale = float(gl_r.abs().max())
     torch.testing.assert_close(gl_f, gl_r, rtol=1e-4, atol=1e-5 * scale)
     assert float(gl_f[:16].abs().max()) <= 1e-5 * scale  # clamped log-prob + one-point entropy: no gradient
+
+
+@pytest.mark.parametrize("density", [0.02, 0.3])
+def test_fused_ppo_loss_bf16_inputs_equal_cast_path(cuda, density):
+    """bb_ppo_loss_*_bf16 (bf16 logits / values, as the autocast network outputs them) == the fp32 loss on the same
+    values widened, then its gradients cast to bf16 (autograd's casts around the fp32 loss): the loss and the
+    metrics bit for bit, d/dlogits and d/dvalues bit for bit."""
+    from agents.ppo import PPOConfig
+    from runtime.kernels import PPOLossFunction
+
+    torch.manual_seed(7 + int(density * 100))
+    B = 2048
+    cfg = PPOConfig()
+    lb = (torch.randn(B, 192, device=cuda) * 3).to(torch.bfloat16)
+    vb = torch.randn(B, device=cuda).to(torch.bfloat16)
+    mask = (torch.rand(B, 192, device=cuda) < density).float()
+    mask[torch.arange(B, device=cuda), torch.randint(0, 192, (B,), device=cuda)] = 1.0
+    actions = torch.multinomial(mask, 1).squeeze(1)
+    old = -torch.rand(B, device=cuda) * 4
+    adv, ret = torch.randn(B, device=cuda), torch.randn(B, device=cuda)
+    res = []
+    for bf16 in (True, False):
+        lg = lb.clone().requires_grad_(True)
+        vg = vb.clone().requires_grad_(True)
+        x, v = (lg, vg) if bf16 else (lg.float(), vg.float())  # the cast path: autograd casts the gradients back
+        loss, stats = PPOLossFunction.apply(x, v, mask, actions, old, adv, ret, cfg.clip_epsilon, cfg.value_coef,
+                                            cfg.entropy_coef)
+        loss.backward()
+        assert lg.grad.dtype == torch.bfloat16 and vg.grad.dtype == torch.bfloat16
+        res.append((loss.detach(), stats, lg.grad, vg.grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
