@@ -706,6 +706,10 @@ class PPOAgent(BaseAgent):
         with torch.no_grad():
             params = [p.detach().clone() for p in self.network.parameters()]
             bufs = [b.detach().clone() for b in self.network.buffers()]
+            # the Linear tails' dropout generator word too, so the first replay draws the masks the first
+            # eager step would have (models/network.py _dropout_rng)
+            rng = self.network._dropout_rng(self.device) if hasattr(self.network, "_dropout_rng") else None
+            rng0 = rng.clone() if rng is not None else None
             opt = {p: {k: v.detach().clone() for k, v in st.items() if torch.is_tensor(v)}
                    for p, st in self.optimizer.state.items()}
         dev_stream = torch.cuda.current_stream(self.device)
@@ -769,6 +773,8 @@ class PPOAgent(BaseAgent):
                 p.copy_(v)
             for b, v in zip(self.network.buffers(), bufs):
                 b.copy_(v)
+            if rng is not None:
+                rng.copy_(rng0)
             for p, st in self.optimizer.state.items():
                 old = opt.get(p)
                 for k, v in st.items():

@@ -929,3 +929,28 @@ extern "C" int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const
   return BB_OK;
 }
 
+extern "C" int bb_dropout_forward(void* d_y, int64_t n, float p, int64_t* d_rng, void* stream) {
+  if (!d_y || !d_rng) return fail(nullptr, BB_ERR_ARG, "bb_dropout_forward: NULL argument");
+  if (n <= 0 || n % 8) return fail(nullptr, BB_ERR_ARG, "bb_dropout_forward: n must be a positive multiple of 8");
+  if (!(p > 0.f && p < 1.f)) return fail(nullptr, BB_ERR_ARG, "bb_dropout_forward: p must be in (0, 1)");
+  hipError_t st = launch_dropout_fwd(d_y, n, p, d_rng, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue) return fail(nullptr, BB_ERR_ARG, "bb_dropout_forward: y must be 16-byte aligned");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_dropout_forward");
+  return BB_OK;
+}
+
+extern "C" int64_t bb_linear_bgrad_workspace_bytes(int32_t rows, int32_t cols) {
+  return linear_bgrad_workspace_bytes(rows, cols);
+}
+
+extern "C" int32_t bb_linear_bgrad_counters(int32_t cols) { return linear_bgrad_counters(cols); }
+
+extern "C" int bb_linear_bgrad(const void* d_dy, const void* d_yd, int32_t rows, int32_t cols, float scale, void* d_g,
+                               void* d_db, float* d_ws, uint32_t* d_cnt, void* stream) {
+  if (!d_dy || !d_db || (d_yd && !d_g) || !d_ws || !d_cnt)
+    return fail(nullptr, BB_ERR_ARG, "bb_linear_bgrad: NULL argument");
+  if (rows <= 0 || cols <= 0) return fail(nullptr, BB_ERR_ARG, "bb_linear_bgrad: rows and cols must be positive");
+  hipError_t st = launch_linear_bgrad(d_dy, d_yd, rows, cols, scale, d_g, d_db, d_ws, d_cnt, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_bgrad");
+  return BB_OK;
+}

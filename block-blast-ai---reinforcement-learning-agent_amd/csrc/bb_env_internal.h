@@ -146,6 +146,13 @@ hipError_t launch_adam_clip(int count, float* const* p, float* const* g, float* 
                             float max_norm, double* ws, float* norm_out, hipStream_t s);
 hipError_t launch_cast_multi(int count, int dir, const void* const* src, void* const* dst, const int64_t* n,
                              const int32_t* perm_c, const int32_t* perm_hw, hipStream_t s);
+// bf16 Linear tails (bb_optim.hip): in-place dropout with a self-advancing device generator word, and the
+// masked-scale + ReLU-mask + bias-gradient pass of the backward
+hipError_t launch_dropout_fwd(void* y, int64_t n, float p, int64_t* rng, hipStream_t s);
+int64_t linear_bgrad_workspace_bytes(int rows, int cols);
+int linear_bgrad_counters(int cols);
+hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int cols, float scale, void* g, void* db,
+                               float* part, uint32_t* cnt, hipStream_t s);
 
 // Host helpers (bb_tables.cpp).
 void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces]);

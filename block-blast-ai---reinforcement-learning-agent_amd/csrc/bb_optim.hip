@@ -27,9 +27,22 @@
 // cast_multi_kernel does all tensors of one direction in one launch; a tensor
 // with perm_c > 0 is [O][perm_c][perm_hw] on the f32 side and [O][perm_hw][perm_c]
 // on the bf16 side (transposed per row through LDS, both sides coalesced).
+//
+// Linear tails under bf16 autocast (network.py:89-117, nn.Linear -> nn.ReLU -> nn.Dropout(0.1)):
+//   dropout_fwd_kernel  : nn.Dropout's training forward over the ReLU GEMM's bf16 output, in place
+//                         (y * scale where a Philox4x32-10 draw keeps the element, else 0); the generator's
+//                         (seed, offset) live in a device word the launch advances itself, so a captured
+//                         HIP graph draws fresh masks on every replay without a host-side refill;
+//   linear_bgrad_kernel : the backward up to the GEMMs -- g = dy * scale where the saved output
+//                         (after ReLU and dropout) is > 0, else 0 (dropout's masked scale, then
+//                         threshold_backward, as autograd rounds them), and the bias gradient
+//                         db = sum over rows of g (f32 sums in a fixed order, bf16 out) -- one pass
+//                         instead of torch's masked-scale, threshold, semaphore memset and reduction.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <math.h>
+
+#include <algorithm>
 
 #include "bb_env_internal.h"
 
@@ -260,6 +273,217 @@ __global__ void __launch_bounds__(kOptThreads) cast_multi_kernel(const CastTable
   }
 }
 
+// ---------------------------------------------------------------- Linear tails (dropout, bias gradient)
+constexpr int kDropThreads = 256;  // 8 bf16 per thread per pass
+#ifndef BB_DROP_BLOCKS
+#define BB_DROP_BLOCKS 128
+#endif
+constexpr int kDropMaxBlocks = BB_DROP_BLOCKS;
+#ifndef BB_DROP_UNROLL
+#define BB_DROP_UNROLL 4
+#endif
+constexpr int kDropUnroll = BB_DROP_UNROLL;
+// linear_bgrad_kernel shape: BB_BGRAD_CFG 0 = 64 columns x 32 row lanes (256 threads), row chunks of ~128 rows
+// (BB_BGRAD_CHUNK)
+// with the write-through hand-off; 1 = 8 columns x 1024 row lanes, all rows in one workgroup; 2 = 16 columns x
+// 512 row lanes, all rows; 3 = 8 columns x 256 row lanes, row chunks of ~512 rows with the hand-off
+#ifndef BB_BGRAD_CFG
+#define BB_BGRAD_CFG 0
+#endif
+constexpr int kBgradCL = BB_BGRAD_CFG == 0 ? 8 : BB_BGRAD_CFG == 2 ? 2 : 1;  // column lanes of 8 columns
+constexpr int kBgradThreads = BB_BGRAD_CFG == 0 || BB_BGRAD_CFG == 3 ? 256 : 1024;
+constexpr int kBgradCols = 8 * kBgradCL;
+#ifndef BB_BGRAD_CHUNK
+#define BB_BGRAD_CHUNK 128
+#endif
+constexpr int kBgradChunk = BB_BGRAD_CFG == 0 ? BB_BGRAD_CHUNK : BB_BGRAD_CFG == 3 ? 512 : 0;  // rows per chunk
+constexpr int kBgradMaxSplit = 64;
+
+// Write-through hand-off (MI355X_MICROARCH.md, fence-free form): partial sums stored with agent-scope relaxed
+// atomic stores (sc1, written through to L2), the storing wave drains them (s_waitcnt vmcnt(0)), a barrier,
+// then one lane counts the workgroup on an agent-scope counter; the workgroup whose add returns the last count
+// reads every partial with agent-scope loads.
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) uint32_t guint32;
+__device__ __forceinline__ void wt_store(float* p, float v) {
+  __hip_atomic_store((gfloat*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float wt_load(const float* p) {
+  return __hip_atomic_load((const gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t wt_arrive(uint32_t* c) {
+  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+struct Philox4 {
+  uint32_t v[4];
+};
+
+// Philox4x32-10 (Salmon et al., SC'11): counter c, key k.
+__device__ __forceinline__ Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                                 uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return Philox4{{c0, c1, c2, c3}};
+}
+
+// rng: {seed, offset, arrivals, 0} (int64).  Element i keeps its value when draw (i / 4, lane i % 4) of
+// counter (i / 4, offset) >= thresh (P(drop) = thresh / 2^32).  The last workgroup to arrive advances the
+// offset by one and clears the arrival count, so the next launch (or graph replay) draws a new mask.
+__global__ void __launch_bounds__(kDropThreads) dropout_fwd_kernel(uint16_t* y, int64_t n, uint32_t thresh,
+                                                                   float scale, int64_t* rng) {
+  const uint64_t seed = (uint64_t)rng[0], off = (uint64_t)rng[1];
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32), o0 = (uint32_t)off, o1 = (uint32_t)(off >> 32);
+  // kDropUnroll vectors of 8 per thread in flight: loads first (y is read and written in place, so the
+  // compiler would not hoist the next vector's load above this one's store)
+  const int64_t stride = (int64_t)gridDim.x * kDropThreads * 8;
+  for (int64_t i0 = ((int64_t)blockIdx.x * kDropThreads + threadIdx.x) * 8; i0 < n; i0 += stride * kDropUnroll) {
+    uint4 h[kDropUnroll];
+#pragma unroll
+    for (int u = 0; u < kDropUnroll; ++u)
+      if (i0 + u * stride < n) h[u] = *reinterpret_cast<const uint4*>(y + i0 + u * stride);
+#pragma unroll
+    for (int u = 0; u < kDropUnroll; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n) break;
+      const uint64_t q = (uint64_t)i >> 2;
+      const Philox4 a = philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), o0, o1, k0, k1);
+      const Philox4 b = philox4x32_10((uint32_t)(q + 1), (uint32_t)((q + 1) >> 32), o0, o1, k0, k1);
+      const uint32_t r[8] = {a.v[0], a.v[1], a.v[2], a.v[3], b.v[0], b.v[1], b.v[2], b.v[3]};
+      uint32_t w[4] = {h[u].x, h[u].y, h[u].z, h[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint16_t lo = r[2 * k] >= thresh ? f2bf_rne(bf2f((uint16_t)w[k]) * scale) : 0;
+        const uint16_t hi = r[2 * k + 1] >= thresh ? f2bf_rne(bf2f((uint16_t)(w[k] >> 16)) * scale) : 0;
+        w[k] = (uint32_t)lo | ((uint32_t)hi << 16);
+      }
+      *reinterpret_cast<uint4*>(y + i) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  __syncthreads();  // every thread's (seed, offset) load has returned before the block counts itself
+  if (threadIdx.x == 0) {
+    const uint64_t prev = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(rng + 2), 1ull,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (uint64_t)gridDim.x - 1) {  // the last block: every block has read the offset
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(rng + 1), (unsigned long long)(off + 1),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(rng + 2), 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Grid (column blocks of kBgradCols, row chunks): kBgradCL column lanes x 8 columns, the rest row lanes; each
+// thread's 8 column sums over its chunk's rows in row order, a wave's row lanes added by a fixed xor tree, the
+// waves in wave order (LDS).  One chunk: those are db.  Several: each chunk publishes its partial sums
+// (write-through) and the last chunk of a column block to arrive adds them in chunk order (deterministic
+// whatever the arrival order), writes db and re-arms the block's counter (cnt: zero between launches).
+// yd == nullptr: g is dy itself (not written).  VEC: cols % 8 == 0 and 16-byte aligned rows.
+template <bool VEC>
+__global__ void __launch_bounds__(kBgradThreads) linear_bgrad_kernel(const uint16_t* __restrict__ dy,
+                                                                      const uint16_t* __restrict__ yd, int rows,
+                                                                      int cols, int chunk_rows, float scale,
+                                                                      uint16_t* __restrict__ g,
+                                                                      uint16_t* __restrict__ db, float* part,
+                                                                      uint32_t* cnt) {
+  constexpr int RL = kBgradThreads / kBgradCL;
+  __shared__ float wsum[kBgradThreads / 64][kBgradCols];
+  const int cl = threadIdx.x % kBgradCL, rl = threadIdx.x / kBgradCL;
+  const int c0 = blockIdx.x * kBgradCols + cl * 8;
+  const int r0 = blockIdx.y * chunk_rows, r1 = min(rows, r0 + chunk_rows);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (VEC) {
+    if (c0 < cols) {
+#pragma unroll 4
+      for (int r = r0 + rl; r < r1; r += RL) {
+        const int64_t o = (int64_t)r * cols + c0;
+        const uint4 h = *reinterpret_cast<const uint4*>(dy + o);
+        uint32_t w[4] = {h.x, h.y, h.z, h.w};
+        if (yd) {
+          const uint4 m = *reinterpret_cast<const uint4*>(yd + o);
+          const uint32_t mm[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            // bf16 > 0: sign clear and not +0
+            const uint16_t lo = ((int16_t)(mm[k] & 0xffffu) > 0) ? f2bf_rne(bf2f((uint16_t)w[k]) * scale) : 0;
+            const uint16_t hi = ((int16_t)(mm[k] >> 16) > 0) ? f2bf_rne(bf2f((uint16_t)(w[k] >> 16)) * scale) : 0;
+            w[k] = (uint32_t)lo | ((uint32_t)hi << 16);
+          }
+          *reinterpret_cast<uint4*>(g + o) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] += bf2f((uint16_t)w[k]);
+          acc[2 * k + 1] += bf2f((uint16_t)(w[k] >> 16));
+        }
+      }
+    }
+  } else {
+    for (int r = r0 + rl; r < r1; r += RL) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        if (c < cols) {
+          const int64_t o = (int64_t)r * cols + c;
+          uint16_t v = dy[o];
+          if (yd) {
+            v = ((int16_t)yd[o] > 0) ? f2bf_rne(bf2f(v) * scale) : 0;
+            g[o] = v;
+          }
+          acc[j] += bf2f(v);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int m = kBgradCL; m < 64; m <<= 1) acc[j] += __shfl_xor(acc[j], m, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane < kBgradCL)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wsum[wave][lane * 8 + j] = acc[j];
+  __syncthreads();
+  const int nsplit = gridDim.y;
+  if (threadIdx.x >= kBgradCols) return;
+  const int c = blockIdx.x * kBgradCols + threadIdx.x;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kBgradThreads / 64; ++k) s += wsum[k][threadIdx.x];
+  if (nsplit == 1) {
+    if (c < cols) db[c] = f2bf_rne(s);
+    return;
+  }
+  // (the threads left are one wave: kBgradCols <= 64)
+  float* col = part + (size_t)blockIdx.x * nsplit * kBgradCols + threadIdx.x;
+  wt_store(col + (size_t)blockIdx.y * kBgradCols, s);
+  wt_drain();
+  int arrived = 0;
+  if (threadIdx.x == 0) arrived = wt_arrive(cnt + blockIdx.x) == (uint32_t)(nsplit - 1);
+  if (!__shfl(arrived, 0, 64)) return;  // lane 0's add has returned
+  float v[kBgradMaxSplit];
+#pragma unroll
+  for (int k = 0; k < kBgradMaxSplit; ++k) v[k] = k < nsplit ? wt_load(col + (size_t)k * kBgradCols) : 0.f;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < kBgradMaxSplit; ++k) t += v[k];  // chunk order; absent chunks add +0
+  if (c < cols) db[c] = f2bf_rne(t);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = 0u;  // every chunk has counted itself: re-armed for the next launch
+}
+
 int build_adam_table(AdamTable& tab, int count, float* const* p, float* const* g, float* const* m, float* const* v,
                      float* const* step, const int64_t* n) {
   if (count <= 0 || count > kOptMaxTensors) return -1;
@@ -331,6 +555,50 @@ hipError_t launch_cast_multi(int count, int dir, const void* const* src, void* c
     hipLaunchKernelGGL(cast_multi_kernel<0>, dim3(c), dim3(kOptThreads), 0, s, tab);
   else
     hipLaunchKernelGGL(cast_multi_kernel<1>, dim3(c), dim3(kOptThreads), 0, s, tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_dropout_fwd(void* y, int64_t n, float p, int64_t* rng, hipStream_t s) {
+  if (n <= 0 || n % 8 || !y || !rng || !(p > 0.f && p < 1.f) || (reinterpret_cast<uintptr_t>(y) & 15))
+    return hipErrorInvalidValue;
+  // torch's fused dropout: scale = 1 / (1 - p) with 1 - p held as a float
+  const float keep = (float)(1.0 - (double)p);
+  const float scale = (float)(1.0 / (double)keep);
+  const double t = (double)p * 4294967296.0;
+  const uint32_t thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  int64_t blocks = (n / 8 + kDropThreads - 1) / kDropThreads;
+  if (blocks > kDropMaxBlocks) blocks = kDropMaxBlocks;  // grid-stride: few arrivals on the generator word
+  hipLaunchKernelGGL(dropout_fwd_kernel, dim3((unsigned)blocks), dim3(kDropThreads), 0, s, (uint16_t*)y, n,
+                     thresh, scale, rng);
+  return hipGetLastError();
+}
+
+static int bgrad_split(int rows) {
+  return kBgradChunk ? std::min(kBgradMaxSplit, (rows + kBgradChunk - 1) / kBgradChunk) : 1;
+}
+
+int64_t linear_bgrad_workspace_bytes(int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return -1;
+  return ((cols + kBgradCols - 1) / kBgradCols) * (int64_t)bgrad_split(rows) * kBgradCols * (int64_t)sizeof(float);
+}
+
+int linear_bgrad_counters(int cols) { return cols > 0 ? (cols + kBgradCols - 1) / kBgradCols : -1; }
+
+hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int cols, float scale, void* g, void* db,
+                               float* part, uint32_t* cnt, hipStream_t s) {
+  if (rows <= 0 || cols <= 0 || !dy || !db || (yd && !g) || !part || !cnt) return hipErrorInvalidValue;
+  const bool vec = cols % 8 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(yd) | reinterpret_cast<uintptr_t>(g)) &
+                    15) == 0;
+  const int nsplit = bgrad_split(rows);
+  const int chunk = (rows + nsplit - 1) / nsplit;
+  const dim3 grid((cols + kBgradCols - 1) / kBgradCols, nsplit);
+  if (vec)
+    hipLaunchKernelGGL(linear_bgrad_kernel<true>, grid, dim3(kBgradThreads), 0, s, (const uint16_t*)dy,
+                       (const uint16_t*)yd, rows, cols, chunk, scale, (uint16_t*)g, (uint16_t*)db, part, cnt);
+  else
+    hipLaunchKernelGGL(linear_bgrad_kernel<false>, grid, dim3(kBgradThreads), 0, s, (const uint16_t*)dy,
+                       (const uint16_t*)yd, rows, cols, chunk, scale, (uint16_t*)g, (uint16_t*)db, part, cnt);
   return hipGetLastError();
 }
 

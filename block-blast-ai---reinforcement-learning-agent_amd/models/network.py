@@ -287,26 +287,58 @@ class BlockBlastNetwork(nn.Module):
             k += 2 if has_b else 1
         return sh
 
-    @staticmethod
-    def _run(seq: nn.Sequential, z: torch.Tensor, sh, skip_first: bool = False, relu_first: bool = False) -> torch.Tensor:
+    def _dropout_after(self, mods, i: int, z: torch.Tensor):
+        """(p, rng) when mods[i] is an nn.Dropout the bf16 Linear tail applies itself (bb_dropout_forward),
+        else None.  p = 0 in eval mode (nothing drawn)."""
+        from runtime.kernels import LINEAR_TAIL
+
+        if not (LINEAR_TAIL and i < len(mods) and isinstance(mods[i], nn.Dropout) and z.is_cuda):
+            return None
+        d = mods[i]
+        p = float(d.p) if d.training else 0.0
+        if not 0.0 <= p < 1.0:
+            return None
+        return p, (self._dropout_rng(z.device) if p > 0.0 else None)
+
+    def _dropout_rng(self, dev: torch.device) -> torch.Tensor:
+        """The device generator word {seed, offset, 0, 0} of bb_dropout_forward (one per network and
+        device; the launches advance the offset).  Seeded from torch.initial_seed(), so torch.manual_seed
+        reproduces the masks.  Made outside graph capture (the first training step's eager run)."""
+        rngs = self.__dict__.setdefault("_drop_rngs", {})
+        dev = torch.device(dev)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        key = str(dev)
+        if key not in rngs:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("BlockBlastNetwork: run one eager training step before capturing (dropout state)")
+            seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + len(rngs) + 1) & ((1 << 63) - 1)
+            rngs[key] = torch.tensor([seed, 0, 0, 0], dtype=torch.int64, device=dev)
+        return rngs[key]
+
+    def _run(self, seq: nn.Sequential, z: torch.Tensor, sh, skip: int = 0) -> torch.Tensor:
         """seq(z), its Linear layers on the bf16 shadows ``sh`` when given; a
         Linear followed by a ReLU then runs as one GEMM with the ReLU in its
-        epilogue (LinearReLUFunction).  skip_first: seq[0] was applied already
-        (relu_first: with the following ReLU)."""
+        epilogue (LinearReLUFunction), with a following Dropout applied by the same
+        function.  skip: modules seq[:skip] were applied already."""
         mods = list(seq)
-        i = 1 if skip_first else 0
-        if skip_first and relu_first:
-            i = 2
+        i = skip
         while i < len(mods):
             m = mods[i]
             if sh is not None and isinstance(m, nn.Linear):
                 if LINEAR_RELU and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU) and z.dim() == 2:
                     from runtime.kernels import LinearReLUFunction
 
-                    z = LinearReLUFunction.apply(z, *sh[m])
-                    i += 2
+                    drop = self._dropout_after(mods, i + 2, z)
+                    z = LinearReLUFunction.apply(z, *sh[m], *(drop or ()))
+                    i += 3 if drop is not None else 2
                     continue
-                z = F.linear(z, *sh[m])
+                from runtime import kernels as K
+
+                if K.LINEAR_TAIL and z.dim() == 2 and sh[m][1] is not None:
+                    z = K.LinearBiasFunction.apply(z, *sh[m])
+                else:
+                    z = F.linear(z, *sh[m])
             elif isinstance(m, nn.Linear):
                 z = _linear(z, m)
             else:
@@ -347,19 +379,22 @@ class BlockBlastNetwork(nn.Module):
             flat = h.permute(0, 2, 3, 1).reshape(n, hh * ww * c)
             sh = self._linear_shadows(h, (c, hh * ww))
             if sh is not None:  # the permuted bf16 weight comes out of the multi-tensor cast
-                fuse = LINEAR_RELU and len(self.fc_encoder) > 1 and isinstance(self.fc_encoder[1], nn.ReLU)
+                mods = list(self.fc_encoder)
+                fuse = LINEAR_RELU and len(mods) > 1 and isinstance(mods[1], nn.ReLU)
                 if fuse:
                     from runtime.kernels import LinearReLUFunction
 
-                    z = LinearReLUFunction.apply(flat, *sh[lin0])
+                    drop = self._dropout_after(mods, 2, flat)
+                    z = LinearReLUFunction.apply(flat, *sh[lin0], *(drop or ()))
+                    skip = 3 if drop is not None else 2
                 else:
-                    z = F.linear(flat, *sh[lin0])
-                return self._run(self.fc_encoder, z, sh, skip_first=True, relu_first=fuse), sh
+                    z, skip = F.linear(flat, *sh[lin0]), 1
+                return self._run(self.fc_encoder, z, sh, skip), sh
             wp = lin0.weight.view(o, c, hh, ww).permute(0, 2, 3, 1)
             if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
                 wp = wp.to(torch.bfloat16, memory_format=torch.contiguous_format)  # autocast's cast + the permute, one pass
             w = wp.reshape(o, hh * ww * c)
-            return self._run(self.fc_encoder, _linear(flat, lin0, w), None, skip_first=True), None
+            return self._run(self.fc_encoder, _linear(flat, lin0, w), None, 1), None
         sh = self._linear_shadows(h, None)
         return self._run(self.fc_encoder, h.reshape(h.shape[0], -1), sh), sh
 

@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import struct
 from typing import Optional, Tuple
 
 import torch
@@ -622,25 +623,102 @@ def cast_multi(dir_: int, srcs, dsts, perms) -> None:
             "bb_cast_multi")
 
 
+# bf16 Linear tails on bb_dropout_forward / bb_linear_bgrad (0: torch's dropout, threshold_backward and bias
+# reductions, for A/B)
+LINEAR_TAIL = os.environ.get("BB_LINEAR_TAIL", "1") != "0"
+
+
+def _bgrad_ok(t: torch.Tensor) -> bool:
+    return LINEAR_TAIL and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous()
+
+
+_bgrad_cnt = {}  # (device, stream) -> zeroed uint32 counters of bb_linear_bgrad (re-armed by every launch)
+_BGRAD_CNT = 4096
+
+
+def _bgrad_counters(dev: torch.device, cols: int) -> torch.Tensor:
+    lib = L.load()
+    need = lib.bb_linear_bgrad_counters(cols)
+    if need > _BGRAD_CNT:
+        raise L.BBNativeError(f"linear_bgrad: {cols} columns need {need} counters (> {_BGRAD_CNT})")
+    stream = torch.cuda.current_stream(dev)
+    key = (str(dev), stream.cuda_stream)
+    cnt = _bgrad_cnt.get(key)
+    if cnt is None:
+        if torch.cuda.is_current_stream_capturing():  # zeroed outside capture: a captured fill would re-zero
+            raise L.BBNativeError("linear_bgrad: run one eager backward on this stream before capturing")
+        cnt = _bgrad_cnt[key] = torch.zeros(_BGRAD_CNT, dtype=torch.int32, device=dev)
+    return cnt
+
+
+def linear_bgrad(gy: torch.Tensor, yd: Optional[torch.Tensor], scale: float = 1.0):
+    """(g, db) of bb_linear_bgrad: g = gy * scale where yd > 0 else 0 (yd None: g = gy), db = g.sum(0)."""
+    rows, cols = gy.shape
+    dev = gy.device
+    lib = L.load()
+    g = torch.empty_like(gy) if yd is not None else gy
+    db = torch.empty(cols, dtype=gy.dtype, device=dev)
+    ws = torch.empty((lib.bb_linear_bgrad_workspace_bytes(rows, cols) + 3) // 4, dtype=torch.float32, device=dev)
+    cnt = _bgrad_counters(dev, cols)
+    L.check(lib.bb_linear_bgrad(_p(gy), _p(yd) if yd is not None else None, rows, cols, float(scale), _p(g), _p(db),
+                                _p(ws), _p(cnt), _s(dev)), "bb_linear_bgrad")
+    return g, db
+
+
 class LinearReLUFunction(torch.autograd.Function):
-    """relu(F.linear(x, w, b)) for 2-D x with the ReLU in hipBLASLt's GEMM
-    epilogue (torch._addmm_activation; one kernel instead of the GEMM and a
-    clamp pass).  Backward as autograd's: the mask from the saved output
-    (threshold_backward, F.relu's rule), then dx = g w, dw = g^T x, db = sum g."""
+    """dropout(relu(F.linear(x, w, b)), p) for 2-D x: the ReLU in hipBLASLt's GEMM epilogue
+    (torch._addmm_activation), then -- p > 0, nn.Dropout in training -- bb_dropout_forward in place (its
+    Philox generator word ``rng``, advanced on the device by every launch).  Backward: bb_linear_bgrad
+    (dropout's masked scale, threshold_backward from the saved output, the bias gradient's sum: one pass),
+    then dx = g w, dw = g^T x."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, p: float = 0.0, rng: Optional[torch.Tensor] = None):
         y = torch._addmm_activation(bias, x, weight.t())
+        scale = 1.0
+        if p > 0.0:
+            if rng is None or y.numel() % 8 or not _bgrad_ok(y):
+                raise L.BBNativeError("LinearReLUFunction: dropout needs a bf16 output of 8k elements and rng")
+            L.check(L.load().bb_dropout_forward(_p(y), y.numel(), float(p), _p(rng), _s(y.device)),
+                    "bb_dropout_forward")
+            scale = 1.0 / struct.unpack("f", struct.pack("f", 1.0 - p))[0]  # bb_optim.hip launch_dropout_fwd
         ctx.save_for_backward(x, weight, y)
+        ctx.scale = scale
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, weight, y = ctx.saved_tensors
-        g = torch.ops.aten.threshold_backward(gy, y, 0)
-        db = g.sum(0) if ctx.needs_input_grad[2] else None
+        gy = gy.contiguous()
+        if _bgrad_ok(gy) and _bgrad_ok(y) and gy.shape == y.shape:
+            g, db = linear_bgrad(gy, y, ctx.scale)
+        else:  # (f32 / CPU operands: torch's ops; dropout was applied only on the bf16 path)
+            g = torch.ops.aten.threshold_backward(gy, y, 0)
+            db = g.sum(0)
+        db = db if ctx.needs_input_grad[2] else None
         dx = g.mm(weight) if ctx.needs_input_grad[0] else None
         dw = g.t().mm(x) if ctx.needs_input_grad[1] else None
+        return dx, dw, db, None, None
+
+
+class LinearBiasFunction(torch.autograd.Function):
+    """F.linear(x, w, b) for 2-D bf16 x whose backward takes the bias gradient from bb_linear_bgrad (one pass
+    over dy) instead of torch's semaphore memset + reduction."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        return torch.addmm(bias, x, weight.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        db = None
+        if ctx.needs_input_grad[2]:
+            db = linear_bgrad(gy, None)[1] if _bgrad_ok(gy) else gy.sum(0)
+        dx = gy.mm(weight) if ctx.needs_input_grad[0] else None
+        dw = gy.t().mm(x) if ctx.needs_input_grad[1] else None
         return dx, dw, db
 
 

@@ -60,7 +60,7 @@ class Info(C.Structure):
     ]
 
 
-ABI_VERSION = 7  # include/bbvec.h BB_ABI_VERSION
+ABI_VERSION = 8  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -166,6 +166,10 @@ SIGNATURES = {
     "bb_adam_clip_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double, _F,
                                     _P, _P, _P]),
     "bb_cast_multi": (C.c_int, [_I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "bb_dropout_forward": (C.c_int, [_P, C.c_int64, _F, _P, _P]),
+    "bb_linear_bgrad_workspace_bytes": (C.c_int64, [_I32, _I32]),
+    "bb_linear_bgrad_counters": (C.c_int32, [_I32]),
+    "bb_linear_bgrad": (C.c_int, [_P, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),
 }
 
 # the env entry points, which the host backend (libbbvec_host.so) exports too

@@ -32,12 +32,13 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 7  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
+#define BB_ABI_VERSION 8  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
                               4: bb_conv_in_* and bb_relu_bias_grad* removed;
                               5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed;
                               6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
                                  bb_conv3x3_f32_prep / _forward, bb_linear_f32;
-                              7: bb_ppo_loss_forward_bf16 / _backward_bf16 */
+                              7: bb_ppo_loss_forward_bf16 / _backward_bf16;
+                              8: bb_dropout_forward, bb_linear_bgrad */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -443,6 +444,28 @@ int bb_adam_clip_step(int32_t num_tensors, float* const* h_param, float* const* 
  * first FC weight against a channels_last flatten); perm_c * perm_hw <= 8192. */
 int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const* h_src, void* const* h_dst,
                   const int64_t* h_numel, const int32_t* h_perm_c, const int32_t* h_perm_hw, void* stream);
+
+/* The CNN's bf16 Linear tails (network.py:89-117: nn.Linear -> nn.ReLU -> nn.Dropout under autocast), not
+ * part of the env boundary.
+ * bb_dropout_forward: nn.Dropout(p)'s training forward, in place over n bf16 values (n % 8 == 0, 16-byte
+ * aligned): y * (1 / (1 - p)) where the element is kept, else 0.  Element i is dropped when draw i % 4 of
+ * Philox4x32-10(counter = (i / 4, offset), key = seed) is below p * 2^32.  d_rng is a device int64[4]
+ * {seed, offset, 0, 0}: the launch reads (seed, offset), and the last of its workgroups advances offset by
+ * one (words 2-3 are its scratch and stay 0 between launches), so every launch -- and every replay of a
+ * captured graph -- draws a new mask.  One launch.
+ * bb_linear_bgrad: the backward of y = dropout(relu(x w^T + b)) up to its GEMMs.  d_yd = the saved output
+ * (bf16 [rows][cols]): g = dy * scale where yd > 0, else 0 (scale = the dropout's 1 / (1 - p), or 1), written
+ * to d_g; d_yd = NULL: g = dy (plain Linear, nothing written).  d_db[c] = sum over rows of g[., c], f32 sums
+ * in a fixed order rounded to bf16 (deterministic).  One launch: row chunks of 64 columns each publish
+ * partial sums to d_ws (bb_linear_bgrad_workspace_bytes(rows, cols) bytes) and the last chunk to finish adds
+ * them; d_cnt holds bb_linear_bgrad_counters(cols) uint32 counters that must be zero before the first launch
+ * and are zero again after each (the launch re-arms them) -- one counter block per stream: launches that run
+ * concurrently must not share one. */
+int bb_dropout_forward(void* d_y, int64_t n, float p, int64_t* d_rng, void* stream);
+int64_t bb_linear_bgrad_workspace_bytes(int32_t rows, int32_t cols);
+int32_t bb_linear_bgrad_counters(int32_t cols);
+int bb_linear_bgrad(const void* d_dy, const void* d_yd, int32_t rows, int32_t cols, float scale, void* d_g,
+                    void* d_db, float* d_ws, uint32_t* d_cnt, void* stream);
 
 #ifdef __cplusplus
 }

@@ -122,7 +122,10 @@ def test_network_fused_casts_equal_autocast(cuda, monkeypatch):
     same logits, values and parameter gradients as autocast's own casts."""
     import models.network as N
 
-    monkeypatch.setattr(N, "LINEAR_RELU", False)  # the casts alone (the epilogue ReLU has its own test)
+    from runtime import kernels as K
+
+    monkeypatch.setattr(N, "LINEAR_RELU", False)  # the casts alone (the epilogue ReLU has its own test,
+    monkeypatch.setattr(K, "LINEAR_TAIL", False)  # the fused Linear tails theirs: tests/test_gpu_linear_tail.py)
     torch.manual_seed(0)
     net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
     for mod in net.modules():

@@ -93,6 +93,17 @@ VARIANTS = {
     "o2": ["-O2"],
     "ut300": ["-mllvm", "-unroll-threshold=300"],
     "ut1200": ["-mllvm", "-unroll-threshold=1200"],
+    # bb_linear_bgrad shapes (shipped BB_BGRAD_CFG 0, 128-row chunks) and dropout grid caps / loads in flight
+    # (shipped 128 blocks, 4): tools/bench_linear_tail.py, profiles/r05/lt/
+    "bg1": ["-DBB_BGRAD_CFG=1"],
+    "bg2": ["-DBB_BGRAD_CFG=2"],
+    "bg3": ["-DBB_BGRAD_CFG=3"],
+    "bgc32": ["-DBB_BGRAD_CHUNK=32"],
+    "bgc64": ["-DBB_BGRAD_CHUNK=64"],
+    "drop64": ["-DBB_DROP_BLOCKS=64"],
+    "drop256": ["-DBB_DROP_BLOCKS=256"],
+    "drop512": ["-DBB_DROP_BLOCKS=512"],
+    "dropu1": ["-DBB_DROP_UNROLL=1"],
 }
 
 
