@@ -359,7 +359,8 @@ class PPOAgent(BaseAgent):
     def _raw(self, x: torch.Tensor, keep_dtype: bool = False):
         """(logits, value) of the network; under autocast cast to f32 unless keep_dtype (the fused loss reads
         the bf16 outputs as they are: bb_ppo_loss_forward_bf16)."""
-        if self.channels_last and x.is_cuda:
+        bf16_in = self.autocast_dtype == torch.bfloat16 and K.CONV_IN  # the input layer reads either layout
+        if self.channels_last and x.is_cuda and not bf16_in:
             x = x.contiguous(memory_format=torch.channels_last)
         if self.autocast_dtype is not None and x.is_cuda:
             with torch.autocast("cuda", dtype=self.autocast_dtype, cache_enabled=False):

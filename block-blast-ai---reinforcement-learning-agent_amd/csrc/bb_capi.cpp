@@ -954,3 +954,27 @@ extern "C" int bb_linear_bgrad(const void* d_dy, const void* d_yd, int32_t rows,
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_bgrad");
   return BB_OK;
 }
+
+extern "C" int64_t bb_conv_in_wgrad_workspace_bytes(int32_t N) { return conv_in_wgrad_workspace_bytes(N); }
+
+extern "C" int bb_conv_in_forward(const float* d_x, int32_t x_nhwc, const float* d_w, int32_t wl, int32_t N, void* d_y,
+                                  void* stream) {
+  if (!d_x || !d_w || !d_y) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: NULL argument");
+  if (N <= 0) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: N must be positive");
+  hipError_t st = launch_conv_in_forward(d_x, x_nhwc, d_w, wl, N, d_y, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: wl must be 0 or 1, x and y 16-byte aligned");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_forward");
+  return BB_OK;
+}
+
+extern "C" int bb_conv_in_wgrad(const float* d_x, int32_t x_nhwc, const void* d_dy, int32_t N, float* d_ws, int32_t wl,
+                                float* d_dw, void* stream) {
+  if (!d_x || !d_dy || !d_ws || !d_dw) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: NULL argument");
+  if (N <= 0) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: N must be positive");
+  hipError_t st = launch_conv_in_wgrad(d_x, x_nhwc, d_dy, N, d_ws, wl, d_dw, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_wgrad: wl must be 0 or 1, x and dy 16-byte aligned");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_wgrad");
+  return BB_OK;
+}

@@ -24,6 +24,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "bb_env_internal.h"
 
 namespace bb {
@@ -804,6 +806,196 @@ hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, flo
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// The input layer, conv 4 -> 64 (network.py:75-87's first Conv2d) under bf16 autocast: x f32 (the stacked
+// board + piece planes, NCHW or channels_last) and w f32 rounded to bf16 as autocast casts them, products
+// exact, f32 sums, y bf16 NHWC.  K = 36 (k = 4 t + ci) is padded to 64 for mfma_f32_16x16x32_bf16 with
+// A = the weights (M = co), B = the board's im2col (N = pixel): a lane's C values are 4 consecutive output
+// channels of one pixel, staged through LDS so a wave stores its board's 8 KB as whole 16-byte chunks.
+// Weight gradient dw[co][k] = sum_{b,p} dy[b,p,co] x[b,p+d_t,ci]: M = co, N = k (36 -> 48), K = pixels, dy
+// transposed through LDS; a workgroup's partial [t][co][ci] goes to conv_wgrad_reduce (fixed chunk order).
+// ---------------------------------------------------------------------------
+constexpr int kInCout = 64, kInK = 36, kInWaves = 4;
+constexpr int kInWgChunks = 128;  // weight-gradient workgroups (partials) at most
+
+__device__ __forceinline__ bf16x8 pack8(float4 a, float4 b) {
+  bf16x8 r;
+  r[0] = (short)f2bf(a.x); r[1] = (short)f2bf(a.y); r[2] = (short)f2bf(a.z); r[3] = (short)f2bf(a.w);
+  r[4] = (short)f2bf(b.x); r[5] = (short)f2bf(b.y); r[6] = (short)f2bf(b.z); r[7] = (short)f2bf(b.w);
+  return r;
+}
+
+// board b of x -> the wave's zero-haloed [10][10] pixel image of float4 (4 input channels)
+__device__ __forceinline__ void in_load_board(const float* __restrict__ x, int x_nhwc, int b, int lane,
+                                              float4* xpad) {
+  const float4 v = reinterpret_cast<const float4*>(x + (size_t)b * 256)[lane];
+  if (x_nhwc) {  // lane = pixel
+    xpad[((lane >> 3) + 1) * 10 + (lane & 7) + 1] = v;
+  } else {  // lane: channel lane >> 4, pixels 4 (lane & 15) .. + 3
+    const int ci = lane >> 4, p0 = (lane & 15) * 4, r = p0 >> 3, c0 = p0 & 7;
+    float* f = reinterpret_cast<float*>(xpad) + ((r + 1) * 10 + c0 + 1) * 4 + ci;
+    f[0] = v.x;
+    f[4] = v.y;
+    f[8] = v.z;
+    f[12] = v.w;
+  }
+}
+
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__global__ void __launch_bounds__(256) conv_in_fwd_kernel(const float* __restrict__ x, int x_nhwc,
+                                                          const float* __restrict__ w, int wl, int nb,
+                                                          uint16_t* __restrict__ y) {
+  __shared__ float wsh[kInCout * kInK];      // [co][k]
+  __shared__ float4 xpad[kInWaves][100];      // per wave: [(r + 1) * 10 + c + 1] -> 4 channels
+  __shared__ uint4 ost[kInWaves][64 * 8];     // per wave: [pixel][16-B chunk ^ (pixel & 7)] of 8 channels
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
+  for (int i = threadIdx.x; i < kInCout * kInK; i += 256) {
+    const int co = i / kInK, k = i % kInK, t = k >> 2, ci = k & 3;
+    wsh[i] = w[wl ? (co * 9 + t) * 4 + ci : (co * 4 + ci) * 9 + t];
+  }
+  for (int i = lane; i < 100; i += 64) xpad[wave][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  bf16x8 afr[4][2];  // A[co = 16 mt + l16][k = 32 s + 8 g + j]
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s2 + 8 * g + j;
+        afr[mt][s2][j] = (short)(k < kInK ? f2bf(wsh[(16 * mt + l16) * kInK + k]) : 0);
+      }
+  for (int b = blockIdx.x * kInWaves + wave; b < nb; b += gridDim.x * kInWaves) {
+    in_load_board(x, x_nhwc, b, lane, xpad[wave]);
+    lds_wait();
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int p = 16 * nt + l16, r = p >> 3, c = p & 7;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int t0 = 8 * s2 + 2 * g;  // taps t0, t0 + 1 (k = 4 t + ci)
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v0 = t0 < 9 ? xpad[wave][(r + t0 / 3) * 10 + c + t0 % 3] : z;
+        const float4 v1 = t0 + 1 < 9 ? xpad[wave][(r + (t0 + 1) / 3) * 10 + c + (t0 + 1) % 3] : z;
+        const bf16x8 bfr = pack8(v0, v1);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mt][s2], bfr, acc[mt][nt], 0, 0, 0);
+      }
+    }
+    // C[co = 16 mt + 4 g + i][pixel = 16 nt + l16] -> ost (8 bytes: 4 channels)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int p = 16 * nt + l16, chunk = 2 * mt + (g >> 1);
+        uint2 v;
+        v.x = pack2(acc[mt][nt][0], acc[mt][nt][1]);
+        v.y = pack2(acc[mt][nt][2], acc[mt][nt][3]);
+        reinterpret_cast<uint2*>(&ost[wave][p * 8 + (chunk ^ (p & 7))])[g & 1] = v;
+      }
+    lds_wait();
+    uint4* yb = reinterpret_cast<uint4*>(y + (size_t)b * 64 * kInCout);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = lane + 64 * q, p = idx >> 3, ch = idx & 7;
+      yb[idx] = ost[wave][p * 8 + (ch ^ (p & 7))];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) conv_in_wgrad_kernel(const float* __restrict__ x, int x_nhwc,
+                                                            const uint16_t* __restrict__ dy, int nb,
+                                                            float* __restrict__ part) {
+  // per wave: dyT [64 co][64 pixels] bf16 (16-B chunk of 8 pixels at chunk ^ ((co >> 3) & 7)), then the padded
+  // board; after the board loop the same bytes hold waves 1-3's sums for wave 0 to add
+  constexpr int kDyT = 64 * 64 * 2, kXp = 100 * 16, kPerWave = kDyT + kXp;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kInWaves * kPerWave];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
+  uint16_t* dyt = reinterpret_cast<uint16_t*>(smem + wave * kPerWave);
+  float4* xpad = reinterpret_cast<float4*>(smem + wave * kPerWave + kDyT);
+  for (int i = lane; i < 100; i += 64) xpad[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  f32x4 acc[4][3];  // C[co = 16 mt + 4 g + i][k = 16 nt + l16]
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int b = blockIdx.x * kInWaves + wave; b < nb; b += gridDim.x * kInWaves) {
+    const uint4* db = reinterpret_cast<const uint4*>(dy + (size_t)b * 64 * kInCout);
+    uint4 dv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dv[q] = db[lane + 64 * q];
+    in_load_board(x, x_nhwc, b, lane, xpad);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // pixel p, channels 8 ch .. 8 ch + 7 -> dyT[co][p]
+      const int idx = lane + 64 * q, p = idx >> 3, ch = idx & 7;
+      const uint32_t wv[4] = {dv[q].x, dv[q].y, dv[q].z, dv[q].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = 8 * ch + e;
+        dyt[co * 64 + (((p >> 3) ^ ch) << 3) + (p & 7)] = (uint16_t)(e & 1 ? wv[e >> 1] >> 16 : wv[e >> 1]);
+      }
+    }
+    lds_wait();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 afr[4];  // A[co = 16 mt + l16][pixel = 32 s + 8 g + j]
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int co = 16 * mt + l16;
+        afr[mt] = *reinterpret_cast<const bf16x8*>(dyt + co * 64 + (((4 * s2 + g) ^ ((co >> 3) & 7)) << 3));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) {
+        const int k = 16 * nt + l16, t = k >> 2, ci = k & 3, r = 4 * s2 + g;  // pixels (r, 0 .. 7)
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = k < kInK ? reinterpret_cast<const float*>(xpad)[((r + t / 3) * 10 + j + t % 3) * 4 + ci] : 0.f;
+        const bf16x8 bfr = pack8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mt], bfr, acc[mt][nt], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // every wave is done with its LDS images
+  float* red = reinterpret_cast<float*>(smem);  // [3][9][64][4]: waves 1-3
+  constexpr int kW = 9 * kInCout * 4;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) {
+      const int k = 16 * nt + l16, t = k >> 2, ci = k & 3;
+      if (wave > 0 && k < kInK)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[(wave - 1) * kW + (t * kInCout + 16 * mt + 4 * g + i) * 4 + ci] = acc[mt][nt][i];
+    }
+  __syncthreads();
+  if (wave > 0) return;
+  float* out = part + (size_t)blockIdx.x * kW;  // [t][co][ci], conv_wgrad_reduce's chunk layout
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) {
+      const int k = 16 * nt + l16, t = k >> 2, ci = k & 3;
+      if (k < kInK)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int o = (t * kInCout + 16 * mt + 4 * g + i) * 4 + ci;
+          out[o] = ((acc[mt][nt][i] + red[o]) + red[kW + o]) + red[2 * kW + o];  // wave order
+        }
+    }
+}
+
+int in_wgrad_chunks(int nb) { return nb <= 0 ? 0 : std::min(kInWgChunks, (nb + kInWaves - 1) / kInWaves); }
+
 }  // namespace
 
 bool conv3x3_supported(int cin, int cout) {
@@ -859,6 +1051,35 @@ hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, 
   if (cin == 64 && cout == 128) return wgrad_t<64, 128>(x, dy, nb, ws, wl, dw, s);
   if (cin == 128 && cout == 64) return wgrad_t<128, 64>(x, dy, nb, ws, wl, dw, s);
   return wgrad_t<128, 128>(x, dy, nb, ws, wl, dw, s);
+}
+
+int64_t conv_in_wgrad_workspace_bytes(int nb) {
+  return nb > 0 ? (int64_t)in_wgrad_chunks(nb) * 9 * kInCout * 4 * (int64_t)sizeof(float) : -1;
+}
+
+hipError_t launch_conv_in_forward(const float* x, int x_nhwc, const float* w, int wl, int nb, void* y, hipStream_t s) {
+  if (nb <= 0 || !x || !w || !y || (wl != 0 && wl != 1) || (reinterpret_cast<uintptr_t>(x) & 15) ||
+      (reinterpret_cast<uintptr_t>(y) & 15))
+    return hipErrorInvalidValue;
+  const int blocks = std::min((nb + kInWaves - 1) / kInWaves, 4096);
+  hipLaunchKernelGGL(conv_in_fwd_kernel, dim3(blocks), dim3(256), 0, s, x, x_nhwc ? 1 : 0, w, wl, nb, (uint16_t*)y);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_in_wgrad(const float* x, int x_nhwc, const void* dy, int nb, float* ws, int wl, float* dw,
+                                hipStream_t s) {
+  if (nb <= 0 || !x || !dy || !ws || !dw || (wl != 0 && wl != 1) || (reinterpret_cast<uintptr_t>(x) & 15) ||
+      (reinterpret_cast<uintptr_t>(dy) & 15))
+    return hipErrorInvalidValue;
+  const int chunks = in_wgrad_chunks(nb);
+  hipLaunchKernelGGL(conv_in_wgrad_kernel, dim3(chunks), dim3(256), 0, s, x, x_nhwc ? 1 : 0, (const uint16_t*)dy, nb,
+                     ws);
+  hipError_t st = hipGetLastError();
+  if (st != hipSuccess) return st;
+  const int n = 9 * kInCout * 4;
+  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ws, chunks,
+                     kInCout, 4, wl, dw);
+  return hipGetLastError();
 }
 
 }  // namespace bb

@@ -121,6 +121,12 @@ hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin,
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);
 
+// the input layer, conv 4 -> 64 (x f32 NCHW or NHWC, w f32 [64][4][3][3] wl 0 or [64][3][3][4] wl 1)
+int64_t conv_in_wgrad_workspace_bytes(int nb);
+hipError_t launch_conv_in_forward(const float* x, int x_nhwc, const float* w, int wl, int nb, void* y, hipStream_t s);
+hipError_t launch_conv_in_wgrad(const float* x, int x_nhwc, const void* dy, int nb, float* ws, int wl, float* dw,
+                                hipStream_t s);
+
 bool conv3x3_f32_supported(int cin, int cout);
 hipError_t launch_conv3x3_f32_prep(const float* w, int cin, int cout, int wl, float* wf, float* wd, hipStream_t s);
 hipError_t launch_conv3x3_f32_forward(const float* x, const float* w, int nb, int cin, int cout, float* y,

@@ -113,10 +113,12 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> 
     autocast's conv2d.  ``images``: {conv: bf16 weight images} prepared for all
     layers in one launch (BlockBlastNetwork._conv_images)."""
     if _hip_conv_on(x):
-        from runtime.kernels import Conv3x3Function, conv3x3_fusable
+        from runtime.kernels import ConvInFunction, Conv3x3Function, conv3x3_fusable, conv_in_fusable
 
         if conv3x3_fusable(x, conv):
             return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox)
+        if conv_in_fusable(x, conv):  # the 4 -> 64 input layer: f32 boards in, bf16 NHWC out
+            return ConvInFunction.apply(x, conv.weight)
     elif _f32_conv_on(x, conv):
         from runtime.kernels import Conv3x3F32Function
 

@@ -350,6 +350,52 @@ def _w_layout(w: torch.Tensor) -> int:
     raise L.BBNativeError("conv weight must be contiguous or channels_last")
 
 
+# the input layer (conv 4 -> 64) on bb_conv_in_forward / _wgrad under bf16 autocast (0: MIOpen's, for A/B)
+CONV_IN = os.environ.get("BB_CONV_IN", "1") != "0"
+
+
+def conv_in_fusable(x: torch.Tensor, conv) -> bool:
+    """The input layer: an nn.Conv2d 4 -> 64, 3x3 / stride 1 / pad 1, on f32 8x8 boards (NCHW or channels_last)."""
+    return (CONV_IN and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and x.shape[1:] == (4, 8, 8)
+            and x.shape[0] > 0 and conv.in_channels == 4 and conv.out_channels == 64 and conv.groups == 1
+            and tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1)
+            and tuple(conv.padding) == (1, 1) and tuple(conv.dilation) == (1, 1) and conv.padding_mode == "zeros"
+            and conv.weight.dtype == torch.float32
+            and (x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)))
+
+
+class ConvInFunction(torch.autograd.Function):
+    """conv2d(x, weight, padding=1) without bias for the 4 -> 64 input layer under bf16 autocast: f32 input and
+    weight rounded to bf16 (autocast's casts), f32 sums, bf16 NHWC output; backward: the f32 weight gradient
+    only (the input is data)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        _need_cuda(x, weight)
+        nhwc = 0 if x.is_contiguous() else 1
+        wl = _w_layout(weight)
+        n = x.shape[0]
+        y = torch.empty((n, 64, 8, 8), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        L.check(L.load().bb_conv_in_forward(_p(x), nhwc, _p(weight), wl, n, _p(y), _s(x.device)), "bb_conv_in_forward")
+        ctx.save_for_backward(x, weight)
+        ctx.nhwc, ctx.wl = nhwc, wl
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        if not ctx.needs_input_grad[1]:
+            return None, None
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        n = x.shape[0]
+        lib = L.load()
+        ws = torch.empty((lib.bb_conv_in_wgrad_workspace_bytes(n) + 3) // 4, dtype=torch.float32, device=x.device)
+        dw = torch.empty_like(weight)
+        L.check(lib.bb_conv_in_wgrad(_p(x), ctx.nhwc, _p(dy), n, _p(ws), ctx.wl, _p(dw), _s(x.device)),
+                "bb_conv_in_wgrad")
+        return None, dw
+
+
 class Conv3x3Function(torch.autograd.Function):
     """conv2d(x, weight, padding=1) without bias under bf16 autocast:
     bf16 NHWC activations, f32 accumulation, bf16 output, f32 weight gradient

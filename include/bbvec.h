@@ -38,7 +38,7 @@ extern "C" {
                               6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
                                  bb_conv3x3_f32_prep / _forward, bb_linear_f32;
                               7: bb_ppo_loss_forward_bf16 / _backward_bf16;
-                              8: bb_dropout_forward, bb_linear_bgrad */
+                              8: bb_dropout_forward, bb_linear_bgrad; bb_conv_in_forward / _wgrad */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -462,6 +462,20 @@ int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const* h_src, vo
  * and are zero again after each (the launch re-arms them) -- one counter block per stream: launches that run
  * concurrently must not share one. */
 int bb_dropout_forward(void* d_y, int64_t n, float p, int64_t* d_rng, void* stream);
+
+/* The CNN's input layer, conv 4 -> 64 3x3 pad 1 over 8x8 boards (network.py:75-87, the first nn.Conv2d, without
+ * its bias: the BatchNorm after it adds that) under bf16 autocast, not part of the env boundary.  x: N boards
+ * of f32 [4][8][8] (x_nhwc 0) or [8][8][4] (x_nhwc 1, channels_last), 16-byte aligned; w: f32 [64][4][3][3]
+ * (wl 0) or [64][3][3][4] (wl 1).  x and w are rounded to bf16 as autocast casts them, products summed in f32.
+ * bb_conv_in_forward: y = bf16 [N][8][8][64] (NHWC).  One launch.
+ * bb_conv_in_wgrad: dw (f32, w's layout) = sum over boards and pixels of dy (bf16 NHWC [N][8][8][64]) times
+ * the bf16 input, f32 sums: per-workgroup partials in d_ws (bb_conv_in_wgrad_workspace_bytes(N) bytes) added
+ * in a fixed order (deterministic).  Two launches. */
+int64_t bb_conv_in_wgrad_workspace_bytes(int32_t N);
+int bb_conv_in_forward(const float* d_x, int32_t x_nhwc, const float* d_w, int32_t wl, int32_t N, void* d_y,
+                       void* stream);
+int bb_conv_in_wgrad(const float* d_x, int32_t x_nhwc, const void* d_dy, int32_t N, float* d_ws, int32_t wl,
+                     float* d_dw, void* stream);
 int64_t bb_linear_bgrad_workspace_bytes(int32_t rows, int32_t cols);
 int32_t bb_linear_bgrad_counters(int32_t cols);
 int bb_linear_bgrad(const void* d_dy, const void* d_yd, int32_t rows, int32_t cols, float scale, void* d_g,

@@ -205,3 +205,99 @@ def test_nhwc_flatten_matches_reference_flatten(cuda, lib, autocast):
         if k.endswith(".bias") and params[k[:-5] + ".weight"].dim() == 4:
             continue  # conv biases feed a BatchNorm: true gradient 0, both sides rounding noise
         assert float((ga[k] - gb[k]).norm() / gb[k].norm()) < tol, k
+
+
+@pytest.mark.parametrize("n,x_nhwc,w_layout", [(1, 0, 0), (3, 1, 1), (7, 0, 1), (1000, 1, 0), (2048, 0, 0),
+                                               (4099, 1, 1)])
+def test_conv_in_forward_and_weight_grad(cuda, lib, n, x_nhwc, w_layout):
+    """The 4 -> 64 input layer (bb_conv_in_forward / _wgrad) against torch's f32 convolution of the same bf16
+    values: the stacked board planes (0/1) and random inputs, both memory formats."""
+    from runtime.kernels import ConvInFunction
+
+    g = torch.Generator(device=cuda).manual_seed(7 + n)
+    x = torch.randn((n, 4, 8, 8), device=cuda, generator=g)
+    x[: n // 2] = (x[: n // 2] > 0.3).float()  # board / piece planes
+    if x_nhwc:
+        x = x.contiguous(memory_format=torch.channels_last)
+    w = torch.randn((64, 4, 3, 3), device=cuda, generator=g) * (2.0 / 36) ** 0.5
+    if w_layout:
+        w = w.contiguous(memory_format=torch.channels_last)
+    dy = torch.randn((n, 64, 8, 8), device=cuda, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    xb, wb = x.bfloat16().double(), w.bfloat16().double()
+    wp = w.clone().requires_grad_(True)
+    y = ConvInFunction.apply(x, wp)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    _bf16_close(y, F.conv2d(xb, wb, padding=1), "input-layer forward")
+    y.backward(dy)
+    ref = torch.nn.grad.conv2d_weight(xb, w.shape, dy.double(), padding=1)
+    assert wp.grad.dtype == torch.float32 and wp.grad.stride() == w.stride()
+    err = float((wp.grad.double() - ref).abs().max())
+    assert err <= 1e-5 * float(ref.abs().max()) + 1e-6, err
+    # deterministic: a second backward gives the same bits
+    wp2 = w.clone().requires_grad_(True)
+    ConvInFunction.apply(x, wp2).backward(dy)
+    assert torch.equal(wp.grad, wp2.grad)
+
+
+def test_network_conv_in_equals_miopen(cuda, monkeypatch):
+    """bf16 training forward + backward of the CNN with the input layer on bb_conv_in_* and on MIOpen: logits
+    and values within bf16 rounding; the first layer's weight gradient against the fp64 weight gradient of the
+    same bf16 input and the same output gradient (captured at the BatchNorm's input), each path on its own."""
+    import models.network as N
+    from runtime import kernels as K
+
+    torch.manual_seed(3)
+    net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    net.train()
+    x = (torch.rand((512, 4, 8, 8), device=cuda) < 0.4).float()
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+    conv0, bn0 = net.conv_encoder[0], net.conv_encoder[1]
+    grabbed = {}
+
+    def pre_hook(mod, args):
+        z = args[0]
+        if z.requires_grad:
+            z.register_hook(lambda gz: grabbed.__setitem__("dz", gz.detach().clone()))
+
+    h = bn0.register_forward_pre_hook(pre_hook)
+    res = {}
+    try:
+        for on in (True, False):
+            monkeypatch.setattr(K, "CONV_IN", on)
+            net.load_state_dict(state0)
+            net.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+                lo, va = net.raw(x.contiguous(memory_format=torch.channels_last) if not on else x)
+            (lo.float().square().mean() + va.float().sum()).backward()
+            truth = torch.nn.grad.conv2d_weight(x.double(), conv0.weight.shape, grabbed["dz"].double(), padding=1)
+            res[on] = (lo.detach().float(), va.detach().float(),
+                       {n: p.grad.clone() for n, p in net.named_parameters()}, truth)
+    finally:
+        h.remove()
+    for a, b in ((res[True][0], res[False][0]), (res[True][1], res[False][1])):
+        assert float((a - b).norm() / b.norm()) < 2e-2
+    for on in (True, False):
+        g0, truth = res[on][2]["conv_encoder.0.weight"].double(), res[on][3]
+        rel = float((g0 - truth).norm() / truth.norm())
+        print(f"input-layer weight gradient vs fp64 ({'bb_conv_in' if on else 'MIOpen'}): {rel:.2e} rel L2")
+        if on:
+            assert rel < 1e-4, rel
+    # the rest of the network sees the input layer's output rounded to bf16 from two different f32 sums, and
+    # every later layer rounds to bf16 again: the BatchNorm parameter gradients (sums with heavy cancellation)
+    # move by up to ~20% per tensor (measured), so the check is on the whole gradient and a loose per-tensor
+    # bound that a layout or indexing error (>= 100%) would still break
+    names = [n for n in res[True][2] if not n.startswith("conv_encoder.0.")]
+    a = torch.cat([res[True][2][n].flatten() for n in names])
+    b = torch.cat([res[False][2][n].flatten() for n in names])
+    cos = float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+    rel = float((a - b).norm() / b.norm())
+    print(f"network gradient, bb_conv_in vs MIOpen input layer: cosine {cos:.5f}, rel L2 {rel:.2e}")
+    assert cos > 0.995 and rel < 0.1, (cos, rel)
+    for name in names:
+        gr, ref = res[True][2][name], res[False][2][name]
+        if name.endswith(".bias") and res[True][2][name[:-5] + ".weight"].dim() == 4:
+            continue  # a conv bias before BatchNorm: zero up to noise
+        assert float((gr - ref).norm() / ref.norm().clamp_min(1e-30)) < 0.5, name
