@@ -978,3 +978,20 @@ extern "C" int bb_conv_in_wgrad(const float* d_x, int32_t x_nhwc, const void* d_
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_wgrad");
   return BB_OK;
 }
+
+extern "C" int64_t bb_linear_wgrad_workspace_bytes(int32_t rows, int32_t N, int32_t K) {
+  return linear_wgrad_workspace_bytes(rows, N, K);
+}
+
+extern "C" int32_t bb_linear_wgrad_counters(int32_t N, int32_t K) { return linear_wgrad_counters(N, K); }
+
+extern "C" int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, int32_t N, int32_t K, void* d_dw,
+                               float* d_ws, uint32_t* d_cnt, void* stream) {
+  if (!d_g || !d_x || !d_dw || !d_ws || !d_cnt) return fail(nullptr, BB_ERR_ARG, "bb_linear_wgrad: NULL argument");
+  hipError_t st = launch_linear_wgrad(d_g, d_x, rows, N, K, d_dw, d_ws, d_cnt, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG,
+                "bb_linear_wgrad: 0 < rows <= 16384, N and K multiples of 32, 16-byte aligned rows");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_wgrad");
+  return BB_OK;
+}

@@ -159,6 +159,10 @@ int64_t linear_bgrad_workspace_bytes(int rows, int cols);
 int linear_bgrad_counters(int cols);
 hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int cols, float scale, void* g, void* db,
                                float* part, uint32_t* cnt, hipStream_t s);
+int64_t linear_wgrad_workspace_bytes(int rows, int N, int K);
+int linear_wgrad_counters(int N, int K);
+hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, int K, void* dw, float* part,
+                               uint32_t* cnt, hipStream_t s);
 
 // Host helpers (bb_tables.cpp).
 void build_piece_tables(PieceRow rows[kPieces], uint8_t dtab[kPieces * kPieces]);

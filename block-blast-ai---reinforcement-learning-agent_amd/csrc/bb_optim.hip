@@ -484,6 +484,124 @@ __global__ void __launch_bounds__(kBgradThreads) linear_bgrad_kernel(const uint1
   if (threadIdx.x == 0) cnt[blockIdx.x] = 0u;  // every chunk has counted itself: re-armed for the next launch
 }
 
+// Weight gradient of a bf16 Linear, dW[n][k] = sum_r g[r][n] x[r][k] (autograd's g^T x for the CNN's small
+// FC / head layers, where hipBLASLt's tiles leave all but a few CUs idle over the 2,048-row reduction).
+// Grid (K / 32, N / 32, row splits of 256): a workgroup loads its 256 rows of both 32-column strips at once
+// (8 x 16 B per thread in flight), wave w takes rows 64 w .. 64 w + 63 (mfma_f32_16x16x16_bf16, 2 x 2 tiles);
+// both operands are row-major in HBM and reach the MFMA k-major through ds_read_b64_tr_b16 (lane 4q + p of a
+// 16-lane group addresses row q, columns 4p .. 4p + 3 of its 4 x 16 block).  The 4 waves' sums are added in
+// wave order (LDS, one output per thread per pass); with several splits each publishes its 32 x 32 partial
+// write-through and the last split
+// to arrive adds them in split order (deterministic) and re-arms the tile's counter; the sum is rounded to
+// bf16 once.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+constexpr int kWgT = 32;        // dW tile
+constexpr int kWgSplit = 256;   // rows per workgroup
+constexpr int kWgMaxSplit = 64;
+
+__device__ __forceinline__ s16x4 tr_read(const uint16_t* lds) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lds);
+}
+
+__global__ void __launch_bounds__(256) linear_wgrad_kernel(const uint16_t* __restrict__ g,
+                                                           const uint16_t* __restrict__ x, int rows, int N, int K,
+                                                           uint16_t* __restrict__ dw, float* part, uint32_t* cnt) {
+  __shared__ __attribute__((aligned(16))) uint16_t gs[kWgSplit][kWgT];
+  __shared__ __attribute__((aligned(16))) uint16_t xs[kWgSplit][kWgT];
+  __shared__ float red[4][kWgT * kWgT];
+  __shared__ int last_split;
+  const int n0 = blockIdx.y * kWgT, k0 = blockIdx.x * kWgT, r0 = blockIdx.z * kWgSplit;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  {  // rows r0 + (t >> 2) + 64 u, 16-byte piece t & 3 of each 64-byte strip row
+    const int lr = t >> 2, lp = (t & 3) * 8;
+    uint4 rg[4], rx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + lr + 64 * u;
+      if (r < rows) {
+        rg[u] = *reinterpret_cast<const uint4*>(g + (int64_t)r * N + n0 + lp);
+        rx[u] = *reinterpret_cast<const uint4*>(x + (int64_t)r * K + k0 + lp);
+      } else {
+        rg[u] = make_uint4(0u, 0u, 0u, 0u);
+        rx[u] = rg[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      *reinterpret_cast<uint4*>(&gs[lr + 64 * u][lp]) = rg[u];
+      *reinterpret_cast<uint4*>(&xs[lr + 64 * u][lp]) = rx[u];
+    }
+  }
+  __syncthreads();
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int rrow = 64 * wave + 16 * ks + 4 * grp + q;  // this lane's block row
+    s16x4 af[2], bf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = tr_read(&gs[rrow][16 * i + 4 * p]);  // A[m = n][k = row]
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bf[j] = tr_read(&xs[rrow][16 * j + 4 * p]);  // B[k = row][n = k]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af[i], bf[j], acc[i][j], 0, 0, 0);
+  }
+  // C[m = 4 grp + e][n = li] of tile (i, j) -> LDS; thread t then owns outputs t + 256 u, summed in wave order
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave][(16 * i + 4 * grp + e) * kWgT + 16 * j + li] = acc[i][j][e];
+  __syncthreads();
+  constexpr int kOut = kWgT * kWgT / 256;
+  float v[kOut];
+#pragma unroll
+  for (int u = 0; u < kOut; ++u) {
+    const int o = t + 256 * u;
+    v[u] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+  }
+  const int nsplit = gridDim.z;
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (nsplit > 1) {  // publish, count; the last split adds every split's partial in split order
+    float* tp = part + (size_t)tile * nsplit * (kWgT * kWgT);
+#pragma unroll
+    for (int u = 0; u < kOut; ++u) wt_store(tp + (size_t)blockIdx.z * (kWgT * kWgT) + t + 256 * u, v[u]);
+    wt_drain();
+    __syncthreads();  // every wave's partial stores have drained
+    if (t == 0) last_split = wt_arrive(cnt + tile) == (uint32_t)(nsplit - 1);
+    __syncthreads();
+    if (!last_split) return;
+#pragma unroll
+    for (int u = 0; u < kOut; ++u) {
+      const float* src = tp + t + 256 * u;
+      float sum = 0.f;
+      for (int z0 = 0; z0 < nsplit; z0 += 8) {
+        float ps[8];
+#pragma unroll
+        for (int z = 0; z < 8; ++z) ps[z] = z0 + z < nsplit ? wt_load(src + (size_t)(z0 + z) * (kWgT * kWgT)) : 0.f;
+#pragma unroll
+        for (int z = 0; z < 8; ++z) sum += ps[z];  // split order; absent splits add +0
+      }
+      v[u] = sum;
+    }
+    if (t == 0) cnt[tile] = 0u;  // every split has counted itself: re-armed for the next launch
+  }
+#pragma unroll
+  for (int u = 0; u < kOut; ++u) {
+    const int o = t + 256 * u, m = o / kWgT, n = o % kWgT;
+    dw[(int64_t)(n0 + m) * K + k0 + n] = f2bf_rne(v[u]);
+  }
+}
+
 int build_adam_table(AdamTable& tab, int count, float* const* p, float* const* g, float* const* m, float* const* v,
                      float* const* step, const int64_t* n) {
   if (count <= 0 || count > kOptMaxTensors) return -1;
@@ -599,6 +717,25 @@ hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int col
   else
     hipLaunchKernelGGL(linear_bgrad_kernel<false>, grid, dim3(kBgradThreads), 0, s, (const uint16_t*)dy,
                        (const uint16_t*)yd, rows, cols, chunk, scale, (uint16_t*)g, (uint16_t*)db, part, cnt);
+  return hipGetLastError();
+}
+
+int64_t linear_wgrad_workspace_bytes(int rows, int N, int K) {
+  if (rows <= 0 || N <= 0 || K <= 0 || N % kWgT || K % kWgT) return -1;
+  const int64_t nsplit = (rows + kWgSplit - 1) / kWgSplit;
+  return nsplit > kWgMaxSplit ? -1 : (int64_t)(N / kWgT) * (K / kWgT) * nsplit * kWgT * kWgT * (int64_t)sizeof(float);
+}
+
+int linear_wgrad_counters(int N, int K) { return (N % kWgT || K % kWgT) ? -1 : (N / kWgT) * (K / kWgT); }
+
+hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, int K, void* dw, float* part,
+                               uint32_t* cnt, hipStream_t s) {
+  if (linear_wgrad_workspace_bytes(rows, N, K) < 0 || !g || !x || !dw || !part || !cnt ||
+      ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(x)) & 15))
+    return hipErrorInvalidValue;
+  const int nsplit = (rows + kWgSplit - 1) / kWgSplit;
+  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(K / kWgT, N / kWgT, nsplit), dim3(256), 0, s, (const uint16_t*)g,
+                     (const uint16_t*)x, rows, N, K, (uint16_t*)dw, part, cnt);
   return hipGetLastError();
 }
 

@@ -682,11 +682,11 @@ _bgrad_cnt = {}  # (device, stream) -> zeroed uint32 counters of bb_linear_bgrad
 _BGRAD_CNT = 4096
 
 
-def _bgrad_counters(dev: torch.device, cols: int) -> torch.Tensor:
-    lib = L.load()
-    need = lib.bb_linear_bgrad_counters(cols)
+def _bgrad_counters(dev: torch.device, need: int) -> torch.Tensor:
+    """The stream's zeroed counter block (bb_linear_bgrad / bb_linear_wgrad; launches on one stream are
+    ordered, and each re-arms the counters it used)."""
     if need > _BGRAD_CNT:
-        raise L.BBNativeError(f"linear_bgrad: {cols} columns need {need} counters (> {_BGRAD_CNT})")
+        raise L.BBNativeError(f"linear tails: {need} counters needed (> {_BGRAD_CNT})")
     stream = torch.cuda.current_stream(dev)
     key = (str(dev), stream.cuda_stream)
     cnt = _bgrad_cnt.get(key)
@@ -705,10 +705,29 @@ def linear_bgrad(gy: torch.Tensor, yd: Optional[torch.Tensor], scale: float = 1.
     g = torch.empty_like(gy) if yd is not None else gy
     db = torch.empty(cols, dtype=gy.dtype, device=dev)
     ws = torch.empty((lib.bb_linear_bgrad_workspace_bytes(rows, cols) + 3) // 4, dtype=torch.float32, device=dev)
-    cnt = _bgrad_counters(dev, cols)
+    cnt = _bgrad_counters(dev, lib.bb_linear_bgrad_counters(cols))
     L.check(lib.bb_linear_bgrad(_p(gy), _p(yd) if yd is not None else None, rows, cols, float(scale), _p(g), _p(db),
                                 _p(ws), _p(cnt), _s(dev)), "bb_linear_bgrad")
     return g, db
+
+
+WGRAD_MAX = 512 * 512  # bb_linear_wgrad for weights up to this size (the 8,192-column first FC stays hipBLASLt's)
+
+
+def linear_wgrad(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """g^T x (autograd's weight gradient of F.linear) on bb_linear_wgrad when the shapes fit, else torch's mm."""
+    rows, n = g.shape
+    k = x.shape[1]
+    if (_bgrad_ok(g) and _bgrad_ok(x) and x.shape[0] == rows and n % 32 == 0 and k % 32 == 0 and n * k <= WGRAD_MAX
+            and 0 < rows <= 16384):
+        lib = L.load()
+        dev = g.device
+        dw = torch.empty((n, k), dtype=g.dtype, device=dev)
+        ws = torch.empty((lib.bb_linear_wgrad_workspace_bytes(rows, n, k) + 3) // 4, dtype=torch.float32, device=dev)
+        cnt = _bgrad_counters(dev, lib.bb_linear_wgrad_counters(n, k))
+        L.check(lib.bb_linear_wgrad(_p(g), _p(x), rows, n, k, _p(dw), _p(ws), _p(cnt), _s(dev)), "bb_linear_wgrad")
+        return dw
+    return g.t().mm(x)
 
 
 class LinearReLUFunction(torch.autograd.Function):
@@ -743,7 +762,7 @@ class LinearReLUFunction(torch.autograd.Function):
             db = g.sum(0)
         db = db if ctx.needs_input_grad[2] else None
         dx = g.mm(weight) if ctx.needs_input_grad[0] else None
-        dw = g.t().mm(x) if ctx.needs_input_grad[1] else None
+        dw = linear_wgrad(g, x) if ctx.needs_input_grad[1] else None
         return dx, dw, db, None, None
 
 
@@ -764,7 +783,7 @@ class LinearBiasFunction(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             db = linear_bgrad(gy, None)[1] if _bgrad_ok(gy) else gy.sum(0)
         dx = gy.mm(weight) if ctx.needs_input_grad[0] else None
-        dw = gy.t().mm(x) if ctx.needs_input_grad[1] else None
+        dw = linear_wgrad(gy, x) if ctx.needs_input_grad[1] else None
         return dx, dw, db
 
 

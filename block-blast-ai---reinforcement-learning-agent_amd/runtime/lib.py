@@ -170,6 +170,9 @@ SIGNATURES = {
     "bb_conv_in_wgrad_workspace_bytes": (C.c_int64, [_I32]),
     "bb_conv_in_forward": (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     "bb_conv_in_wgrad": (C.c_int, [_P, _I32, _P, _I32, _P, _I32, _P, _P]),
+    "bb_linear_wgrad_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
+    "bb_linear_wgrad_counters": (C.c_int32, [_I32, _I32]),
+    "bb_linear_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     "bb_linear_bgrad_workspace_bytes": (C.c_int64, [_I32, _I32]),
     "bb_linear_bgrad_counters": (C.c_int32, [_I32]),
     "bb_linear_bgrad": (C.c_int, [_P, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),

@@ -38,7 +38,7 @@ extern "C" {
                               6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
                                  bb_conv3x3_f32_prep / _forward, bb_linear_f32;
                               7: bb_ppo_loss_forward_bf16 / _backward_bf16;
-                              8: bb_dropout_forward, bb_linear_bgrad; bb_conv_in_forward / _wgrad */
+                              8: bb_dropout_forward, bb_linear_bgrad, bb_linear_wgrad; bb_conv_in_forward / _wgrad */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -476,6 +476,16 @@ int bb_conv_in_forward(const float* d_x, int32_t x_nhwc, const float* d_w, int32
                        void* stream);
 int bb_conv_in_wgrad(const float* d_x, int32_t x_nhwc, const void* d_dy, int32_t N, float* d_ws, int32_t wl,
                      float* d_dw, void* stream);
+/* bb_linear_wgrad: a Linear's weight gradient dW = g^T x (g bf16 [rows][N], x bf16 [rows][K], dW bf16 [N][K],
+ * all row-major; N and K multiples of 32, 16-byte aligned rows, rows <= 16384), f32 sums in a fixed order
+ * rounded once (deterministic).  One launch: splits of 256 rows publish 32 x 32 partials to d_ws
+ * (bb_linear_wgrad_workspace_bytes(rows, N, K) bytes) and the last split of a tile adds them; d_cnt: the
+ * bb_linear_wgrad_counters(N, K) uint32 counters, zero before and after each launch (as bb_linear_bgrad's,
+ * and the same counter block may serve both on one stream). */
+int64_t bb_linear_wgrad_workspace_bytes(int32_t rows, int32_t N, int32_t K);
+int32_t bb_linear_wgrad_counters(int32_t N, int32_t K);
+int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, int32_t N, int32_t K, void* d_dw, float* d_ws,
+                    uint32_t* d_cnt, void* stream);
 int64_t bb_linear_bgrad_workspace_bytes(int32_t rows, int32_t cols);
 int32_t bb_linear_bgrad_counters(int32_t cols);
 int bb_linear_bgrad(const void* d_dy, const void* d_yd, int32_t rows, int32_t cols, float scale, void* d_g,

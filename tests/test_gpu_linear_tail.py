@@ -50,6 +50,28 @@ def test_linear_bgrad_matches_torch(cuda, rows, cols, masked, scale):
     assert float((db == ref.sum(0)).float().mean()) > 0.9
 
 
+def _bf16_near(out, ref, what):
+    """bf16 out within one bf16 rounding of the fp64 reference (plus f32 summation noise)."""
+    err = (out.double() - ref).abs()
+    tol = 2.0 ** -8 * ref.abs() + 1e-5 * float(ref.abs().max())
+    assert bool((err <= tol).all()), (what, float((err - tol).max()))
+
+
+@pytest.mark.parametrize("rows,n,k", [(2048, 128, 256), (2048, 192, 256), (2048, 256, 512), (2048, 512, 512),
+                                      (37, 32, 64), (1000, 64, 96), (5, 32, 32)])
+def test_linear_wgrad_matches_fp64(cuda, rows, n, k):
+    """bb_linear_wgrad: g^T x within one bf16 rounding of fp64, deterministic; rows not a multiple of 64."""
+    from runtime import kernels as K
+
+    g0 = torch.Generator(device=cuda).manual_seed(rows + n + k)
+    g = _bf(torch.randn((rows, n), device=cuda, generator=g0))
+    x = _bf(torch.randn((rows, k), device=cuda, generator=g0)).clamp_min(0)
+    dw = K.linear_wgrad(g, x)
+    assert dw.shape == (n, k) and dw.dtype == torch.bfloat16
+    _bf16_near(dw, g.double().t().mm(x.double()), "linear_wgrad")
+    assert torch.equal(dw, K.linear_wgrad(g, x))
+
+
 def _dropout(y, p, rng):
     from runtime import kernels as K
     from runtime import lib as L
@@ -135,7 +157,7 @@ def test_linear_relu_dropout_function(cuda):
     assert abs(frac - 0.1) < 0.01, frac
     g = torch.where(y > 0, _bf(gy.float() * scale), torch.zeros_like(gy))
     assert torch.equal(x.grad, g.mm(w0))
-    assert torch.equal(w.grad, g.t().mm(x0))
+    _bf16_near(w.grad, g.double().t().mm(x0.double()), "dw")
     exact = g.double().sum(0)
     assert bool(((b.grad.double() - exact).abs() <= 2.0 ** -8 * exact.abs() + 1e-5 * g.double().abs().sum(0)).all())
 
