@@ -547,17 +547,27 @@ class PPOAgent(BaseAgent):
             self._seg = cut[0] if len(cut) == 1 else None
         else:
             logits, values = self._raw(x, keep)
-        if self.fused_loss and logits.is_cuda:  # bb_ppo_loss_forward/backward
+        if self.fused_loss and logits.is_cuda:  # bb_ppo_loss_fused (bb_ppo_loss_forward / _backward otherwise)
+            seed = self._seed(logits.device) if torch.is_grad_enabled() and logits.requires_grad else None
             return K.PPOLossFunction.apply(logits, values, masks, actions, old_log_probs, advantages, returns,
-                                           cfg.clip_epsilon, cfg.value_coef, cfg.entropy_coef)
+                                           cfg.clip_epsilon, cfg.value_coef, cfg.entropy_coef, seed)
         return ppo_loss_torch(logits, values, masks, actions, old_log_probs, advantages, returns, cfg)
 
-    def _backward_loss(self, loss: torch.Tensor) -> None:
-        """loss.backward() seeded with a persistent 1.0 (loss.backward() fills a fresh one: one more kernel in every
-        graph replay).  The seed is made by the first (eager) step, before any capture."""
+    def _seed(self, device: torch.device) -> torch.Tensor:
+        """The persistent 1.0 every minibatch loss is backpropagated with (f32, made by the first eager step,
+        before any capture).  The fused loss receives it up front (bb_ppo_loss_fused: forward and backward in one
+        launch) and hands its gradients over when autograd passes this very tensor back."""
         seed = self._loss_seed
-        if seed is None or seed.device != loss.device or seed.dtype != loss.dtype:
-            seed = self._loss_seed = torch.ones((), dtype=loss.dtype, device=loss.device)
+        if seed is None or seed.device != torch.device(device):
+            seed = self._loss_seed = torch.ones((), dtype=torch.float32, device=device)
+        return seed
+
+    def _backward_loss(self, loss: torch.Tensor) -> None:
+        """loss.backward() seeded with the persistent 1.0 (loss.backward() fills a fresh one: one more kernel in
+        every graph replay)."""
+        seed = self._seed(loss.device)
+        if seed.dtype != loss.dtype:
+            seed = seed.to(loss.dtype)
         loss.backward(seed)
 
     def _backward_segments(self, loss: torch.Tensor, world: int) -> None:

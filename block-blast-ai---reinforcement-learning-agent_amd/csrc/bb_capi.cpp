@@ -704,6 +704,23 @@ extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, 
   return BB_OK;
 }
 
+extern "C" int bb_bn_backward_res(const void* d_x, const void* d_dy, const void* d_y, int32_t dtype, int32_t nhwc,
+                                  int32_t N, int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
+                                  const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
+                                  double* d_ws, void* d_dx, float* d_dweight, float* d_dbias, float* d_dpre_bias,
+                                  void* d_gres, void* stream) {
+  int rc = bn_check(dtype, nhwc, N, C, HW);
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_dy || !d_y || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx)
+    return fail(nullptr, BB_ERR_ARG, "bb_bn_backward_res: NULL argument");
+  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
+  hipError_t st = launch_bn_backward(d_x, d_dy, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, d_save_mean,
+                                     d_save_invstd, 0, d_ws, d_dx, d_dweight, d_dbias, d_dpre_bias, (hipStream_t)stream,
+                                     d_y, d_gres);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_backward_res");
+  return BB_OK;
+}
+
 extern "C" int64_t bb_ppo_loss_workspace_bytes(int32_t B) {
   if (B <= 0) return -1;
   return ppo_loss_workspace_bytes(B);
@@ -712,13 +729,14 @@ extern "C" int64_t bb_ppo_loss_workspace_bytes(int32_t B) {
 namespace {
 int loss_forward_impl(const void* d_logits, const void* d_values, int bf16, const float* d_mask,
                       const int64_t* d_actions, const float* d_old_logp, const float* d_adv, const float* d_ret,
-                      int32_t B, float clip, float value_coef, float entropy_coef, double* d_ws, float* d_stats,
-                      float* d_loss, void* stream, const char* what) {
+                      int32_t B, float clip, float value_coef, float entropy_coef, double* d_ws, uint32_t* d_cnt,
+                      float* d_stats, float* d_loss, void* stream, const char* what) {
   if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret || !d_ws ||
-      !d_stats)
+      !d_cnt || !d_stats)
     return fail(nullptr, BB_ERR_ARG, std::string(what) + ": bad arguments");
   hipError_t st = launch_ppo_loss_forward(d_logits, d_values, bf16, d_mask, d_actions, d_old_logp, d_adv, d_ret, B,
-                                          clip, value_coef, entropy_coef, d_ws, d_stats, d_loss, (hipStream_t)stream);
+                                          clip, value_coef, entropy_coef, d_ws, d_cnt, d_stats, d_loss,
+                                          (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(nullptr, st, what);
   return BB_OK;
 }
@@ -741,9 +759,9 @@ int loss_backward_impl(const void* d_logits, const void* d_values, int bf16, con
 extern "C" int bb_ppo_loss_forward(const float* d_logits, const float* d_values, const float* d_mask,
                                    const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
                                    const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
-                                   double* d_ws, float* d_stats, float* d_loss, void* stream) {
+                                   double* d_ws, uint32_t* d_cnt, float* d_stats, float* d_loss, void* stream) {
   return loss_forward_impl(d_logits, d_values, 0, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip, value_coef,
-                           entropy_coef, d_ws, d_stats, d_loss, stream, "bb_ppo_loss_forward");
+                           entropy_coef, d_ws, d_cnt, d_stats, d_loss, stream, "bb_ppo_loss_forward");
 }
 
 extern "C" int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const float* d_mask,
@@ -757,10 +775,25 @@ extern "C" int bb_ppo_loss_backward(const float* d_logits, const float* d_values
 extern "C" int bb_ppo_loss_forward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
                                         const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
                                         const float* d_ret, int32_t B, float clip, float value_coef,
-                                        float entropy_coef, double* d_ws, float* d_stats, float* d_loss,
-                                        void* stream) {
+                                        float entropy_coef, double* d_ws, uint32_t* d_cnt, float* d_stats,
+                                        float* d_loss, void* stream) {
   return loss_forward_impl(d_logits, d_values, 1, d_mask, d_actions, d_old_logp, d_adv, d_ret, B, clip, value_coef,
-                           entropy_coef, d_ws, d_stats, d_loss, stream, "bb_ppo_loss_forward_bf16");
+                           entropy_coef, d_ws, d_cnt, d_stats, d_loss, stream, "bb_ppo_loss_forward_bf16");
+}
+
+extern "C" int bb_ppo_loss_fused(const void* d_logits, const void* d_values, int32_t bf16, const float* d_mask,
+                                 const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
+                                 const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
+                                 const float* d_grad_loss, void* d_dlogits, void* d_dvalues, double* d_ws,
+                                 uint32_t* d_cnt, float* d_stats, float* d_loss, void* stream) {
+  if (B <= 0 || !d_logits || !d_values || !d_mask || !d_actions || !d_old_logp || !d_adv || !d_ret || !d_grad_loss ||
+      !d_dlogits || !d_dvalues || !d_ws || !d_cnt || !d_stats)
+    return fail(nullptr, BB_ERR_ARG, "bb_ppo_loss_fused: bad arguments");
+  hipError_t st = launch_ppo_loss_fused(d_logits, d_values, bf16 ? 1 : 0, d_mask, d_actions, d_old_logp, d_adv, d_ret,
+                                        B, clip, value_coef, entropy_coef, d_grad_loss, d_dlogits, d_dvalues, d_ws,
+                                        d_cnt, d_stats, d_loss, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_ppo_loss_fused");
+  return BB_OK;
 }
 
 extern "C" int bb_ppo_loss_backward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
@@ -993,5 +1026,27 @@ extern "C" int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, i
     return fail(nullptr, BB_ERR_ARG,
                 "bb_linear_wgrad: 0 < rows <= 16384, N and K multiples of 32, 16-byte aligned rows");
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_wgrad");
+  return BB_OK;
+}
+
+extern "C" int64_t bb_linear_n1_workspace_bytes(int32_t rows, int32_t K) { return linear_n1_workspace_bytes(rows, K); }
+
+extern "C" int32_t bb_linear_n1_counters(int32_t K) { return linear_n1_counters(K); }
+
+extern "C" int bb_linear_n1_forward(const void* d_x, const void* d_w, const void* d_b, int32_t rows, int32_t K, void* d_y,
+                                    void* stream) {
+  hipError_t st = launch_linear_n1_forward(d_x, d_w, d_b, rows, K, d_y, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_linear_n1_forward: rows > 0, K a multiple of 8, x / w non-NULL and aligned");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_n1_forward");
+  return BB_OK;
+}
+
+extern "C" int bb_linear_n1_backward(const void* d_gy, const void* d_x, const void* d_w, int32_t rows, int32_t K,
+                                     void* d_dx, void* d_dw, void* d_db, float* d_ws, uint32_t* d_cnt, void* stream) {
+  hipError_t st = launch_linear_n1_backward(d_gy, d_x, d_w, rows, K, d_dx, d_dw, d_db, d_ws, d_cnt, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_linear_n1_backward: rows > 0, K a multiple of 8, aligned non-NULL buffers");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_n1_backward");
   return BB_OK;
 }

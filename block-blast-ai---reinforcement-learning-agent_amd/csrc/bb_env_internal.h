@@ -109,7 +109,8 @@ hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc
                              int64_t* nbt, void* y, hipStream_t s);
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
-                              int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s);
+                              int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s,
+                              const void* mask = nullptr, void* gout = nullptr);
 
 bool conv3x3_supported(int cin, int cout);
 int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout);
@@ -138,12 +139,16 @@ int64_t ppo_loss_workspace_bytes(int B);
 // logits / values (and backward's dlogits / dvalues): f32, or bf16 when bf16 != 0
 hipError_t launch_ppo_loss_forward(const void* logits, const void* values, int bf16, const float* mask,
                                    const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
-                                   int B, float clip, float vcoef, float ecoef, double* ws, float* stats, float* loss,
-                                   hipStream_t s);
+                                   int B, float clip, float vcoef, float ecoef, double* ws, uint32_t* cnt, float* stats,
+                                   float* loss, hipStream_t s);
 hipError_t launch_ppo_loss_backward(const void* logits, const void* values, int bf16, const float* mask,
                                     const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
                                     int B, float clip, float vcoef, float ecoef, const float* gloss, void* dlogits,
                                     void* dvalues, hipStream_t s);
+hipError_t launch_ppo_loss_fused(const void* logits, const void* values, int bf16, const float* mask,
+                                 const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
+                                 int B, float clip, float vcoef, float ecoef, const float* gloss, void* dlogits,
+                                 void* dvalues, double* ws, uint32_t* cnt, float* stats, float* loss, hipStream_t s);
 
 constexpr int kOptMaxTensors = 48;  // == BB_OPT_MAX_TENSORS
 int64_t adam_clip_workspace_bytes(int count, const int64_t* n);
@@ -159,6 +164,12 @@ int64_t linear_bgrad_workspace_bytes(int rows, int cols);
 int linear_bgrad_counters(int cols);
 hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int cols, float scale, void* g, void* db,
                                float* part, uint32_t* cnt, hipStream_t s);
+int64_t linear_n1_workspace_bytes(int rows, int K);
+int linear_n1_counters(int K);
+hipError_t launch_linear_n1_forward(const void* x, const void* w, const void* b, int rows, int K, void* y,
+                                    hipStream_t s);
+hipError_t launch_linear_n1_backward(const void* gy, const void* x, const void* w, int rows, int K, void* dx, void* dw,
+                                     void* db, float* part, uint32_t* cnt, hipStream_t s);
 int64_t linear_wgrad_workspace_bytes(int rows, int N, int K);
 int linear_wgrad_counters(int N, int K);
 hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, int K, void* dw, float* part,

@@ -4,7 +4,9 @@
 //
 // Issued as torch ops the loss is ~45 elementwise / reduction kernels forward
 // and as many backward, each a few microseconds on 2,048 x 192 logits; here it
-// is one wave per minibatch row for each direction plus a one-wave finaliser.
+// is one wave per minibatch row, one launch each way (the last block to finish
+// finalises the statistics), or one launch for both when the caller supplies
+// the loss gradient up front (the graph root's seed: bb_ppo_loss_fused).
 //
 // Per row (torch fp32 semantics, same operation order as the torch path):
 //   p      = softmax(logits + where(mask, 0, -inf))
@@ -122,74 +124,53 @@ __device__ __forceinline__ void row_forward(const void* __restrict__ logits, con
   r.ent = -wsum(h);
 }
 
-template <bool BF>
-__global__ void __launch_bounds__(kLossThreads) ppo_loss_fwd_kernel(
-    const void* __restrict__ logits, const void* __restrict__ values, const float* __restrict__ mask,
-    const int64_t* __restrict__ actions, const float* __restrict__ old_logp, const float* __restrict__ adv,
-    const float* __restrict__ ret, int B, float clip, double* __restrict__ part) {
-  __shared__ double red[kStats][kRowsPerBlock];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double acc[kStats] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < B; row += (int64_t)gridDim.x * kRowsPerBlock) {
-    RowFwd r;
-    row_forward<BF>(logits, mask, row, actions[row], lane, r);
-    const float A = adv[row];
-    const float ratio = expf(__fsub_rn(r.logp, old_logp[row]));
-    const float s1 = __fmul_rn(ratio, A), s2 = __fmul_rn(fminf(fmaxf(ratio, 1.f - clip), 1.f + clip), A);
-    const float dv = __fsub_rn(ldv<BF>(values, row), ret[row]);
-    const float rm1 = __fsub_rn(ratio, 1.f);
-    acc[0] += (double)(-fminf(s1, s2));
-    acc[1] += (double)__fmul_rn(dv, dv);
-    acc[2] += (double)r.ent;
-    acc[3] += (double)__fsub_rn(rm1, logf(ratio));
-    acc[4] += fabsf(rm1) > clip ? 1.0 : 0.0;
-  }
-  if (lane == 0)
-    for (int k = 0; k < kStats; ++k) red[k][w] = acc[k];
-  __syncthreads();
-  if (threadIdx.x < kStats) {
-    double t = 0.0;
-    for (int k = 0; k < kRowsPerBlock; ++k) t += red[threadIdx.x][k];
-    part[(int64_t)blockIdx.x * kStats + threadIdx.x] = t;
-  }
+// Write-through hand-off of the blocks' partial sums (MI355X_MICROARCH.md, fence-free form): stored sc1 by the
+// storing wave, drained, then one lane counts the block; the block whose add returns the last count reads all
+// partials sc1 and finalises.
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) uint32_t guint32;
+__device__ __forceinline__ void wt_store(double* p, double v) {
+  __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ double wt_load(const double* p) {
+  return __hip_atomic_load((const gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t wt_arrive(uint32_t* c) {
+  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // stats = [policy_loss, value_loss, entropy, total_loss, approx_kl, clip_fraction]; loss = stats[3]
-__global__ void ppo_loss_finalize_kernel(const double* __restrict__ part, int nb, int B, float vcoef, float ecoef,
-                                         float* __restrict__ stats, float* __restrict__ loss) {
-  __shared__ double sh[kStats][64];
-  const int lane = threadIdx.x;  // one wave
-  double a[kStats] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int b = lane; b < nb; b += 64)
-    for (int k = 0; k < kStats; ++k) a[k] += part[(int64_t)b * kStats + k];
-  for (int k = 0; k < kStats; ++k) sh[k][lane] = a[k];
-  __syncthreads();
-  if (lane == 0) {
-    float m[kStats];
-    for (int k = 0; k < kStats; ++k) {
-      double t = 0.0;
-      for (int l = 0; l < 64; ++l) t += sh[k][l];
-      m[k] = (float)(t / (double)B);
-    }
-    const float total = __fadd_rn(__fadd_rn(m[0], __fmul_rn(vcoef, m[1])), __fmul_rn(ecoef, -m[2]));
-    stats[0] = m[0];
-    stats[1] = m[1];
-    stats[2] = m[2];
-    stats[3] = total;
-    stats[4] = m[3];
-    stats[5] = m[4];
-    if (loss) loss[0] = total;
-  }
+__device__ __forceinline__ void loss_stats_out(const double t[kStats], int B, float vcoef, float ecoef,
+                                               float* __restrict__ stats, float* __restrict__ loss) {
+  float m[kStats];
+  for (int k = 0; k < kStats; ++k) m[k] = (float)(t[k] / (double)B);
+  const float total = __fadd_rn(__fadd_rn(m[0], __fmul_rn(vcoef, m[1])), __fmul_rn(ecoef, -m[2]));
+  stats[0] = m[0];
+  stats[1] = m[1];
+  stats[2] = m[2];
+  stats[3] = total;
+  stats[4] = m[3];
+  stats[5] = m[4];
+  if (loss) loss[0] = total;
 }
 
-template <bool BF>
-__global__ void __launch_bounds__(kLossThreads) ppo_loss_bwd_kernel(
+// One wave per row.  STATS: the loss terms' fp64 block partials -> part; with cnt, the last block to arrive
+// adds every block's partials (lane b of a wave per block b, b + 64, ...; the lanes and then the waves in a
+// fixed order) and writes stats / loss, re-arming cnt.  GRAD: d loss / d logits, d values for the loss gradient
+// gloss[0] (the backward's formulas; with STATS too, the forward and backward of one minibatch in one launch).
+template <bool BF, bool STATS, bool GRAD>
+__global__ void __launch_bounds__(kLossThreads) ppo_loss_kernel(
     const void* __restrict__ logits, const void* __restrict__ values, const float* __restrict__ mask,
     const int64_t* __restrict__ actions, const float* __restrict__ old_logp, const float* __restrict__ adv,
     const float* __restrict__ ret, int B, float clip, float vcoef, float ecoef, const float* __restrict__ gloss,
-    void* __restrict__ dlogits, void* __restrict__ dvalues) {
+    void* __restrict__ dlogits, void* __restrict__ dvalues, double* __restrict__ part, uint32_t* cnt,
+    float* __restrict__ stats, float* __restrict__ loss) {
+  __shared__ double red[kStats][kRowsPerBlock];
+  __shared__ int last_block;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const float g = gloss[0];
+  double acc[kStats] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  const float g = GRAD ? gloss[0] : 0.f;
   const float invB = 1.f / (float)B;
   for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + w; row < B; row += (int64_t)gridDim.x * kRowsPerBlock) {
     const int64_t a = actions[row];
@@ -198,42 +179,92 @@ __global__ void __launch_bounds__(kLossThreads) ppo_loss_bwd_kernel(
     const float A = adv[row];
     const float ratio = expf(__fsub_rn(r.logp, old_logp[row]));
     const float s1 = __fmul_rn(ratio, A), s2 = __fmul_rn(fminf(fmaxf(ratio, 1.f - clip), 1.f + clip), A);
-    // d loss / d min(s1, s2) = -g / B; torch.min splits ties half/half
-    const float gmin = -g * invB;
-    const float g1 = s1 < s2 ? gmin : (s1 > s2 ? 0.f : 0.5f * gmin);
-    const float g2 = s2 < s1 ? gmin : (s2 > s1 ? 0.f : 0.5f * gmin);
-    const bool in_clip = ratio >= 1.f - clip && ratio <= 1.f + clip;
-    const float glogp = (g1 * A + (in_clip ? g2 * A : 0.f)) * ratio;  // d exp(x)/dx = exp(x)
-    if (lane == 0) stv<BF>(dvalues, row, vcoef * g * invB * 2.f * __fsub_rn(ldv<BF>(values, row), ret[row]));  // mse
-    const float gent = -ecoef * g * invB;  // ecoef * (-mean(ent))
-    // log(clamp(P_a, eps, 1 - eps)): passes where eps <= P_a <= 1 - eps, divided by the clamped value
-    const float gPa = (r.pa >= kEps32 && r.pa <= 1.f - kEps32) ? glogp / r.pa : 0.f;
-    // P = p / s: gp_k = [k == a] gPa / s - gPa p_a / s^2
-    const int aj = (int)(a >> 6), al = (int)(a & 63);
-    const float p_a = __shfl(aj == 0 ? r.p[0] : (aj == 1 ? r.p[1] : r.p[2]), al);
-    const float corr = gPa * p_a / (r.s * r.s);
-    // entropy = -sum m q log(clamp(q, 1e-10)), q = m p / clamp(ms, 1e-10):
-    //   d/dq_j = -m_j (log(clamp(q_j)) + [q_j >= 1e-10])
-    float gq[3], sgqm = 0.f;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      gq[j] = 0.f;
-      if (r.valid[j]) gq[j] = -gent * (logf(fmaxf(r.q[j], 1e-10f)) + (r.q[j] >= 1e-10f ? 1.f : 0.f));
-      sgqm += r.valid[j] ? gq[j] * r.p[j] : 0.f;
+    if (STATS) {
+      const float dv = __fsub_rn(ldv<BF>(values, row), ret[row]);
+      const float rm1 = __fsub_rn(ratio, 1.f);
+      acc[0] += (double)(-fminf(s1, s2));
+      acc[1] += (double)__fmul_rn(dv, dv);
+      acc[2] += (double)r.ent;
+      acc[3] += (double)__fsub_rn(rm1, logf(ratio));
+      acc[4] += fabsf(rm1) > clip ? 1.0 : 0.0;
     }
-    sgqm = wsum(sgqm);
-    const float gms = r.ms_raw >= 1e-10f ? -sgqm / (r.ms * r.ms) : 0.f;
-    float gp[3], dot = 0.f;
+    if (GRAD) {
+      // d loss / d min(s1, s2) = -g / B; torch.min splits ties half/half
+      const float gmin = -g * invB;
+      const float g1 = s1 < s2 ? gmin : (s1 > s2 ? 0.f : 0.5f * gmin);
+      const float g2 = s2 < s1 ? gmin : (s2 > s1 ? 0.f : 0.5f * gmin);
+      const bool in_clip = ratio >= 1.f - clip && ratio <= 1.f + clip;
+      const float glogp = (g1 * A + (in_clip ? g2 * A : 0.f)) * ratio;  // d exp(x)/dx = exp(x)
+      if (lane == 0) stv<BF>(dvalues, row, vcoef * g * invB * 2.f * __fsub_rn(ldv<BF>(values, row), ret[row]));  // mse
+      const float gent = -ecoef * g * invB;  // ecoef * (-mean(ent))
+      // log(clamp(P_a, eps, 1 - eps)): passes where eps <= P_a <= 1 - eps, divided by the clamped value
+      const float gPa = (r.pa >= kEps32 && r.pa <= 1.f - kEps32) ? glogp / r.pa : 0.f;
+      // P = p / s: gp_k = [k == a] gPa / s - gPa p_a / s^2
+      const int aj = (int)(a >> 6), al = (int)(a & 63);
+      const float p_a = __shfl(aj == 0 ? r.p[0] : (aj == 1 ? r.p[1] : r.p[2]), al);
+      const float corr = gPa * p_a / (r.s * r.s);
+      // entropy = -sum m q log(clamp(q, 1e-10)), q = m p / clamp(ms, 1e-10):
+      //   d/dq_j = -m_j (log(clamp(q_j)) + [q_j >= 1e-10])
+      float gq[3], sgqm = 0.f;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      gp[j] = ((j == aj && lane == al) ? gPa / r.s : 0.f) - corr;
-      if (r.valid[j]) gp[j] += gq[j] / r.ms + gms;
-      dot += gp[j] * r.p[j];
+      for (int j = 0; j < 3; ++j) {
+        gq[j] = 0.f;
+        if (r.valid[j]) gq[j] = -gent * (logf(fmaxf(r.q[j], 1e-10f)) + (r.q[j] >= 1e-10f ? 1.f : 0.f));
+        sgqm += r.valid[j] ? gq[j] * r.p[j] : 0.f;
+      }
+      sgqm = wsum(sgqm);
+      const float gms = r.ms_raw >= 1e-10f ? -sgqm / (r.ms * r.ms) : 0.f;
+      float gp[3], dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        gp[j] = ((j == aj && lane == al) ? gPa / r.s : 0.f) - corr;
+        if (r.valid[j]) gp[j] += gq[j] / r.ms + gms;
+        dot += gp[j] * r.p[j];
+      }
+      dot = wsum(dot);
+      // softmax backward: dz_k = p_k (gp_k - sum_j gp_j p_j); masked entries have p = 0
+#pragma unroll
+      for (int j = 0; j < 3; ++j) stv<BF>(dlogits, row * 192 + j * 64 + lane, r.p[j] * (gp[j] - dot));
     }
-    dot = wsum(dot);
-    // softmax backward: dz_k = p_k (gp_k - sum_j gp_j p_j); masked entries have p = 0
+  }
+  if (!STATS) return;
+  if (lane == 0)
+    for (int k = 0; k < kStats; ++k) red[k][w] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < kStats) {
+    double t = 0.0;
+    for (int k = 0; k < kRowsPerBlock; ++k) t += red[threadIdx.x][k];
+    wt_store(part + (int64_t)blockIdx.x * kStats + threadIdx.x, t);
+    wt_drain();
+  }
+  __syncthreads();  // wave 0's partial stores have drained
+  if (threadIdx.x == 0) last_block = wt_arrive(cnt) == (uint32_t)(gridDim.x - 1);
+  __syncthreads();
+  if (!last_block) return;
+  // every block's partials: lane l of wave k adds blocks (l + 64 j) for stat k (waves 0-3 take stats 0-3, wave 0
+  // then stat 4), the lanes' sums in lane order through LDS
+  __shared__ double lsum[kStats][64];
+  const int nb = gridDim.x;
+  for (int k = w; k < kStats; k += kLossThreads / 64) {
+    double t = 0.0;
+    for (int b0 = lane; b0 < nb; b0 += 8 * 64) {
+      double v[8];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) stv<BF>(dlogits, row * 192 + j * 64 + lane, r.p[j] * (gp[j] - dot));
+      for (int j = 0; j < 8; ++j) v[j] = b0 + 64 * j < nb ? wt_load(part + (int64_t)(b0 + 64 * j) * kStats + k) : 0.0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t += v[j];
+    }
+    lsum[k][lane] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[kStats];
+    for (int k = 0; k < kStats; ++k) {
+      t[k] = 0.0;
+      for (int l = 0; l < 64; ++l) t[k] += lsum[k][l];
+    }
+    loss_stats_out(t, B, vcoef, ecoef, stats, loss);
+    cnt[0] = 0u;  // every block has counted itself: re-armed for the next launch
   }
 }
 
@@ -246,18 +277,21 @@ int loss_blocks(int B) {
 
 int64_t ppo_loss_workspace_bytes(int B) { return (int64_t)sizeof(double) * kStats * loss_blocks(B); }
 
+// stats / loss from one launch: block partials summed by the last block to arrive (cnt: a zeroed counter)
 hipError_t launch_ppo_loss_forward(const void* logits, const void* values, int bf16, const float* mask,
                                    const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
-                                   int B, float clip, float vcoef, float ecoef, double* ws, float* stats, float* loss,
-                                   hipStream_t s) {
+                                   int B, float clip, float vcoef, float ecoef, double* ws, uint32_t* cnt, float* stats,
+                                   float* loss, hipStream_t s) {
+  if (B <= 0 || !cnt) return hipErrorInvalidValue;
   const int nb = loss_blocks(B);
   if (bf16)
-    hipLaunchKernelGGL(ppo_loss_fwd_kernel<true>, dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask, actions,
-                       old_logp, adv, ret, B, clip, ws);
+    hipLaunchKernelGGL((ppo_loss_kernel<true, true, false>), dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask,
+                       actions, old_logp, adv, ret, B, clip, vcoef, ecoef, nullptr, nullptr, nullptr, ws, cnt, stats,
+                       loss);
   else
-    hipLaunchKernelGGL(ppo_loss_fwd_kernel<false>, dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask, actions,
-                       old_logp, adv, ret, B, clip, ws);
-  hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(64), 0, s, ws, nb, B, vcoef, ecoef, stats, loss);
+    hipLaunchKernelGGL((ppo_loss_kernel<false, true, false>), dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask,
+                       actions, old_logp, adv, ret, B, clip, vcoef, ecoef, nullptr, nullptr, nullptr, ws, cnt, stats,
+                       loss);
   return hipGetLastError();
 }
 
@@ -265,12 +299,32 @@ hipError_t launch_ppo_loss_backward(const void* logits, const void* values, int 
                                     const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
                                     int B, float clip, float vcoef, float ecoef, const float* gloss, void* dlogits,
                                     void* dvalues, hipStream_t s) {
+  if (B <= 0) return hipErrorInvalidValue;
   if (bf16)
-    hipLaunchKernelGGL(ppo_loss_bwd_kernel<true>, dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits, values, mask,
-                       actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues);
+    hipLaunchKernelGGL((ppo_loss_kernel<true, false, true>), dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits,
+                       values, mask, actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues,
+                       nullptr, nullptr, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(ppo_loss_bwd_kernel<false>, dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits, values,
-                       mask, actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues);
+    hipLaunchKernelGGL((ppo_loss_kernel<false, false, true>), dim3(loss_blocks(B)), dim3(kLossThreads), 0, s, logits,
+                       values, mask, actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues,
+                       nullptr, nullptr, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_loss_fused(const void* logits, const void* values, int bf16, const float* mask,
+                                 const int64_t* actions, const float* old_logp, const float* adv, const float* ret,
+                                 int B, float clip, float vcoef, float ecoef, const float* gloss, void* dlogits,
+                                 void* dvalues, double* ws, uint32_t* cnt, float* stats, float* loss, hipStream_t s) {
+  if (B <= 0 || !cnt) return hipErrorInvalidValue;
+  const int nb = loss_blocks(B);
+  if (bf16)
+    hipLaunchKernelGGL((ppo_loss_kernel<true, true, true>), dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask,
+                       actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues, ws, cnt, stats,
+                       loss);
+  else
+    hipLaunchKernelGGL((ppo_loss_kernel<false, true, true>), dim3(nb), dim3(kLossThreads), 0, s, logits, values, mask,
+                       actions, old_logp, adv, ret, B, clip, vcoef, ecoef, gloss, dlogits, dvalues, ws, cnt, stats,
+                       loss);
   return hipGetLastError();
 }
 

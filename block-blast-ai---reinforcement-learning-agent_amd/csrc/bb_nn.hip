@@ -97,6 +97,17 @@ struct Vec<__hip_bfloat16> {
   }
 };
 
+// The ReLU of a block's output applied to its gradient from the saved output (torch's threshold_backward,
+// F.relu's rule): g = y > 0 ? dy : 0 -- the ResidualBlock tail, whose ReLU follows the residual add, so the
+// mask cannot be recomputed from the BatchNorm input alone.
+template <typename T>
+__device__ __forceinline__ void mask_grad(const void* mask, int64_t i, float* fg) {
+  float fm[Vec<T>::N];
+  Vec<T>::load(mask, i, fm);
+#pragma unroll
+  for (int j = 0; j < Vec<T>::N; ++j) fg[j] = fm[j] > 0.f ? fg[j] : 0.f;
+}
+
 // Per-channel coefficients of the reduction passes (forward reads only pb).
 struct ChanCoef {
   float pb, mu, is, sc, sh;
@@ -144,12 +155,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // NCHW reduction, block (c, s): channel c, images s, s + S, ... -> part[s][c][kQ].
-template <typename T, bool BWD>
+template <typename T, bool BWD, bool MASK = false>
 __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restrict__ x, const void* __restrict__ dy,
                                                              int N, int C, int HW, const float* __restrict__ pre_bias,
                                                              const float* __restrict__ w, const float* __restrict__ b,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd, int relu,
+                                                             const void* __restrict__ mask,
                                                              double* __restrict__ part) {
   __shared__ double red[kQ][kBnThreads / 64];
   constexpr int V = Vec<T>::N;
@@ -165,6 +177,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
       float fx[V], fg[V];
       Vec<T>::load(x, i, fx);
       if (BWD) Vec<T>::load(dy, i, fg);
+      if (BWD && MASK) mask_grad<T>(mask, i, fg);
 #pragma unroll
       for (int j = 0; j < V; ++j) accumulate<T, BWD>(fx[j], BWD ? fg[j] : 0.f, k, relu, s, q, t);
     }
@@ -184,12 +197,13 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
 // NHWC reduction: thread t owns the V channels of chunk t % cpr of rows
 // t / cpr, t / cpr + rows_per_iter, ... (cpr = C / V divides kBnThreads, so
 // its channels never change); block b writes part[b][c][kQ] for every c.
-template <typename T, bool BWD>
+template <typename T, bool BWD, bool MASK = false>
 __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restrict__ x, const void* __restrict__ dy,
                                                              int R, int C, const float* __restrict__ pre_bias,
                                                              const float* __restrict__ w, const float* __restrict__ b,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd, int relu,
+                                                             const void* __restrict__ mask,
                                                              double* __restrict__ part) {
   constexpr int V = Vec<T>::N;
   constexpr int NQ = BWD ? kQ : 2;  // the forward has no third quantity
@@ -213,6 +227,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
       if (n < R) {
         Vec<T>::load(x, (int64_t)n * cpr + kc, fx[u]);
         if (BWD) Vec<T>::load(dy, (int64_t)n * cpr + kc, fg[u]);
+        if (BWD && MASK) mask_grad<T>(mask, (int64_t)n * cpr + kc, fg[u]);
       }
     }
 #pragma unroll
@@ -362,10 +377,11 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restric
   }
 }
 
-template <typename T, bool NHWC>
+template <typename T, bool NHWC, bool MASK = false>
 __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restrict__ x, const void* __restrict__ dy,
                                                            void* __restrict__ dx, int64_t total, int C, int cpr,
-                                                           int relu, const float* __restrict__ coef) {
+                                                           int relu, const float* __restrict__ coef,
+                                                           const void* __restrict__ mask, void* __restrict__ gout) {
   constexpr int V = Vec<T>::N;
   constexpr int NC = NHWC ? V : 1;
   const float4* cf = reinterpret_cast<const float4*>(coef);
@@ -388,6 +404,10 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restric
     float fx[V], fg[V];
     Vec<T>::load(x, i, fx);
     Vec<T>::load(dy, i, fg);
+    if (MASK) {
+      mask_grad<T>(mask, i, fg);
+      if (gout) Vec<T>::store(gout, i, fg);  // the residual's gradient (values of dy or 0: exact in T)
+    }
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float4& a = k0[NHWC ? j : 0];  // {pb, mu, sc, sh}
@@ -449,13 +469,22 @@ int grid_for_elems(int64_t chunks, int nhwc) {
 template <typename T, bool BWD>
 void launch_reduce(const Plan& p, int nhwc, const void* x, const void* dy, int N, int C, int HW, const float* pb,
                    const float* w, const float* b, const float* mean, const float* invstd, int relu, double* part,
-                   hipStream_t s) {
-  if (nhwc)
-    hipLaunchKernelGGL((bn_reduce_nhwc<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N * HW, C, pb, w, b, mean,
-                       invstd, relu, part);
-  else
-    hipLaunchKernelGGL((bn_reduce_nchw<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N, C, HW, pb, w, b, mean,
-                       invstd, relu, part);
+                   hipStream_t s, const void* mask = nullptr) {
+  if (nhwc) {
+    if (BWD && mask)
+      hipLaunchKernelGGL((bn_reduce_nhwc<T, BWD, true>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N * HW, C, pb, w, b,
+                         mean, invstd, relu, mask, part);
+    else
+      hipLaunchKernelGGL((bn_reduce_nhwc<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N * HW, C, pb, w, b, mean,
+                         invstd, relu, nullptr, part);
+  } else {
+    if (BWD && mask)
+      hipLaunchKernelGGL((bn_reduce_nchw<T, BWD, true>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N, C, HW, pb, w, b,
+                         mean, invstd, relu, mask, part);
+    else
+      hipLaunchKernelGGL((bn_reduce_nchw<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N, C, HW, pb, w, b, mean,
+                         invstd, relu, nullptr, part);
+  }
 }
 
 // Workspace (16-byte aligned): coefficients [C][kCoef] floats (float4 loads),
@@ -493,19 +522,25 @@ hipError_t bn_forward_t(const void* x, const void* res, int nhwc, int N, int C, 
 template <typename T>
 hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, int HW, const float* pb,
                          const float* w, const float* b, const float* mean, const float* invstd, int relu, double* ws,
-                         void* dx, float* dw, float* db, float* dpb, hipStream_t s) {
+                         void* dx, float* dw, float* db, float* dpb, hipStream_t s, const void* mask, void* gout) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
-  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s);
+  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s, mask);
   hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, k.part, p.nb, C, (double)N * HW, pb,
                      w, b, mean, invstd, dw, db, dpb, k.coef);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
-  if (nhwc)
+  if (nhwc && mask)
+    hipLaunchKernelGGL((bn_apply_bwd<T, true, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
+                       k.coef, mask, gout);
+  else if (nhwc)
     hipLaunchKernelGGL((bn_apply_bwd<T, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
-                       k.coef);
+                       k.coef, nullptr, nullptr);
+  else if (mask)
+    hipLaunchKernelGGL((bn_apply_bwd<T, false, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
+                       k.coef, mask, gout);
   else
     hipLaunchKernelGGL((bn_apply_bwd<T, false>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
-                       k.coef);
+                       k.coef, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -529,10 +564,12 @@ hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc
 
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
-                              int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s) {
+                              int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s,
+                              const void* mask, void* gout) {
   if (dtype == 1)
-    return bn_backward_t<__hip_bfloat16>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s);
-  return bn_backward_t<float>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s);
+    return bn_backward_t<__hip_bfloat16>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s,
+                                         mask, gout);
+  return bn_backward_t<float>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s, mask, gout);
 }
 
 }  // namespace bb

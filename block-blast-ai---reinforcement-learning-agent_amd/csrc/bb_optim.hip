@@ -602,6 +602,123 @@ __global__ void __launch_bounds__(256) linear_wgrad_kernel(const uint16_t* __res
   }
 }
 
+// A bf16 Linear with ONE output (network.py's value head, Linear(128, 1), under autocast): torch runs it as a
+// bias copy + a GEMM forward and a GEMM for dx, a GEMM for dW and a reduction for db backward.
+// linear_n1_fwd_kernel: y[r] = bf16(sum_k x[r][k] w[k] + b), 16 lanes per row (8 columns per load), the lanes'
+// sums added by a fixed xor tree.
+// linear_n1_bwd_kernel: dx[r][k] = bf16(gy[r] w[k]) (the K = 1 GEMM's exact product, rounded once), dW[k] =
+// sum_r gy[r] x[r][k] and db = sum_r gy[r] in f32, laid out as bb_linear_bgrad (64 columns x row chunks,
+// write-through partials, the last chunk adds them in chunk order; db is column block 0's 65th sum).
+constexpr int kN1Rows = 16;
+constexpr int kN1Slots = kBgradCols + 1;
+
+__global__ void __launch_bounds__(256) linear_n1_fwd_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ w,
+                                                            const uint16_t* __restrict__ b, int rows, int K,
+                                                            uint16_t* __restrict__ y) {
+  const int r = blockIdx.x * kN1Rows + (threadIdx.x >> 4), l = threadIdx.x & 15;
+  float s = 0.f;
+  if (r < rows)
+    for (int k = 8 * l; k < K; k += 128) {
+      const uint4 xv = *reinterpret_cast<const uint4*>(x + (int64_t)r * K + k);
+      const uint4 wv = *reinterpret_cast<const uint4*>(w + k);
+      const uint32_t xa[4] = {xv.x, xv.y, xv.z, xv.w}, wa[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s += bf2f((uint16_t)xa[e]) * bf2f((uint16_t)wa[e]);
+        s += bf2f((uint16_t)(xa[e] >> 16)) * bf2f((uint16_t)(wa[e] >> 16));
+      }
+    }
+#pragma unroll
+  for (int m = 8; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (l == 0 && r < rows) y[r] = f2bf_rne(s + (b ? bf2f(b[0]) : 0.f));
+}
+
+__global__ void __launch_bounds__(256) linear_n1_bwd_kernel(const uint16_t* __restrict__ gy,
+                                                            const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ w, int rows, int K,
+                                                            int chunk_rows, uint16_t* __restrict__ dx,
+                                                            uint16_t* __restrict__ dw, uint16_t* __restrict__ db,
+                                                            float* part, uint32_t* cnt) {
+  __shared__ float wsum[4][kN1Slots];
+  __shared__ int last_chunk;
+  const int t = threadIdx.x, cl = t & 7, rl = t >> 3, lane = t & 63, wave = t >> 6;
+  const int c0 = blockIdx.x * kBgradCols + cl * 8;
+  const int r0 = blockIdx.y * chunk_rows, r1 = min(rows, r0 + chunk_rows);
+  const bool live = c0 < K;
+  float wv[8], acc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) acc[j] = 0.f;
+  if (live) {
+    const uint4 h = *reinterpret_cast<const uint4*>(w + c0);
+    const uint32_t ha[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      wv[2 * e] = bf2f((uint16_t)ha[e]);
+      wv[2 * e + 1] = bf2f((uint16_t)(ha[e] >> 16));
+    }
+  }
+#pragma unroll 2
+  for (int r = r0 + rl; r < r1; r += 32) {
+    const float gv = bf2f(gy[r]);
+    acc[8] += gv;
+    if (live) {
+      const int64_t o = (int64_t)r * K + c0;
+      const uint4 h = *reinterpret_cast<const uint4*>(x + o);
+      const uint32_t xa[4] = {h.x, h.y, h.z, h.w};
+      uint32_t d[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f((uint16_t)xa[e]), hi = bf2f((uint16_t)(xa[e] >> 16));
+        acc[2 * e] += gv * lo;
+        acc[2 * e + 1] += gv * hi;
+        d[e] = (uint32_t)f2bf_rne(gv * wv[2 * e]) | ((uint32_t)f2bf_rne(gv * wv[2 * e + 1]) << 16);
+      }
+      *reinterpret_cast<uint4*>(dx + o) = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 9; ++j)
+#pragma unroll
+    for (int m = 8; m < 64; m <<= 1) acc[j] += __shfl_xor(acc[j], m, 64);
+  if (lane < 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wsum[wave][lane * 8 + j] = acc[j];
+    if (lane == 0) wsum[wave][kBgradCols] = acc[8];
+  }
+  __syncthreads();
+  float v = 0.f;
+  if (t < kN1Slots) v = ((wsum[0][t] + wsum[1][t]) + wsum[2][t]) + wsum[3][t];  // wave order
+  const int nsplit = gridDim.y;
+  if (nsplit > 1) {
+    float* col = part + (size_t)blockIdx.x * nsplit * kN1Slots + t;
+    if (t < kN1Slots) wt_store(col + (size_t)blockIdx.y * kN1Slots, v);
+    wt_drain();
+    __syncthreads();  // the storing waves have drained
+    if (t == 0) last_chunk = wt_arrive(cnt + blockIdx.x) == (uint32_t)(nsplit - 1);
+    __syncthreads();
+    if (!last_chunk) return;
+    if (t < kN1Slots) {
+      float sum = 0.f;
+      for (int z0 = 0; z0 < nsplit; z0 += 8) {
+        float ps[8];
+#pragma unroll
+        for (int z = 0; z < 8; ++z) ps[z] = z0 + z < nsplit ? wt_load(col + (size_t)(z0 + z) * kN1Slots) : 0.f;
+#pragma unroll
+        for (int z = 0; z < 8; ++z) sum += ps[z];  // chunk order
+      }
+      v = sum;
+    }
+    if (t == 0) cnt[blockIdx.x] = 0u;
+  }
+  if (t < kBgradCols) {
+    const int c = blockIdx.x * kBgradCols + t;
+    if (c < K) dw[c] = f2bf_rne(v);
+  } else if (t == kBgradCols && blockIdx.x == 0 && db) {
+    db[0] = f2bf_rne(v);
+  }
+}
+
 int build_adam_table(AdamTable& tab, int count, float* const* p, float* const* g, float* const* m, float* const* v,
                      float* const* step, const int64_t* n) {
   if (count <= 0 || count > kOptMaxTensors) return -1;
@@ -736,6 +853,36 @@ hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, in
   const int nsplit = (rows + kWgSplit - 1) / kWgSplit;
   hipLaunchKernelGGL(linear_wgrad_kernel, dim3(K / kWgT, N / kWgT, nsplit), dim3(256), 0, s, (const uint16_t*)g,
                      (const uint16_t*)x, rows, N, K, (uint16_t*)dw, part, cnt);
+  return hipGetLastError();
+}
+
+int64_t linear_n1_workspace_bytes(int rows, int K) {
+  if (rows <= 0 || K <= 0 || K % 8) return -1;
+  return (int64_t)((K + kBgradCols - 1) / kBgradCols) * bgrad_split(rows) * kN1Slots * (int64_t)sizeof(float);
+}
+
+int linear_n1_counters(int K) { return K > 0 ? (K + kBgradCols - 1) / kBgradCols : -1; }
+
+hipError_t launch_linear_n1_forward(const void* x, const void* w, const void* b, int rows, int K, void* y,
+                                    hipStream_t s) {
+  if (rows <= 0 || K <= 0 || K % 8 || !x || !w || !y ||
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(linear_n1_fwd_kernel, dim3((rows + kN1Rows - 1) / kN1Rows), dim3(256), 0, s, (const uint16_t*)x,
+                     (const uint16_t*)w, (const uint16_t*)b, rows, K, (uint16_t*)y);
+  return hipGetLastError();
+}
+
+hipError_t launch_linear_n1_backward(const void* gy, const void* x, const void* w, int rows, int K, void* dx, void* dw,
+                                     void* db, float* part, uint32_t* cnt, hipStream_t s) {
+  if (linear_n1_workspace_bytes(rows, K) < 0 || !gy || !x || !w || !dx || !dw || !part || !cnt ||
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dx)) & 15))
+    return hipErrorInvalidValue;
+  const int nsplit = bgrad_split(rows);
+  const int chunk = (rows + nsplit - 1) / nsplit;
+  hipLaunchKernelGGL(linear_n1_bwd_kernel, dim3((K + kBgradCols - 1) / kBgradCols, nsplit), dim3(256), 0, s,
+                     (const uint16_t*)gy, (const uint16_t*)x, (const uint16_t*)w, rows, K, chunk, (uint16_t*)dx,
+                     (uint16_t*)dw, (uint16_t*)db, part, cnt);
   return hipGetLastError();
 }
 

@@ -337,7 +337,9 @@ class BlockBlastNetwork(nn.Module):
                     continue
                 from runtime import kernels as K
 
-                if K.LINEAR_TAIL and z.dim() == 2 and sh[m][1] is not None:
+                if K.LINEAR_TAIL and z.dim() == 2 and K.linear_n1_ok(z, sh[m][0]):
+                    z = K.LinearN1Function.apply(z, *sh[m])  # the value head's one-output layer
+                elif K.LINEAR_TAIL and z.dim() == 2 and sh[m][1] is not None:
                     z = K.LinearBiasFunction.apply(z, *sh[m])
                 else:
                     z = F.linear(z, *sh[m])

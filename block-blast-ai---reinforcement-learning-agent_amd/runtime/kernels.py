@@ -209,13 +209,19 @@ class BatchNormReLUFunction(torch.autograd.Function):
         return dx, dpb, dw, db, None, None, None, None, None, None
 
 
+# ResidualBlock tail backward on bb_bn_backward_res (opt-in: 1.619 against 1.613 ms per step, three interleaved
+# repeats, profiles/r05/rm/ -- the masked passes grow by about what the threshold_backward pass took)
+RES_MASK = os.environ.get("BB_RES_MASK", "0") == "1"
+
+
 class BatchNormAddReLUFunction(torch.autograd.Function):
     """relu(batch_norm(x + pre_bias) + res) with running-stat update: the tail
     of ResidualBlock (network.py:14-30, bn2 -> + identity -> relu) in the
     BatchNorm apply pass (bb_bn_forward_res) instead of two more elementwise
-    passes.  Backward: the ReLU mask from the saved output (torch's
-    threshold_backward, as F.relu's backward), which is also the residual's
-    gradient, then bb_bn_backward without ReLU."""
+    passes.  Backward: bb_bn_backward_res -- the ReLU mask from the saved
+    output (torch's threshold_backward, as F.relu's backward) applied inside
+    the BatchNorm passes, the masked gradient (the residual's) written by the
+    elementwise pass."""
 
     @staticmethod
     def forward(ctx, x, pre_bias, res, weight, bias, running_mean, running_var, momentum: float, eps: float,
@@ -244,7 +250,7 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
     def backward(ctx, dy):
         x, pre_bias, weight, bias, mean, invstd, y = ctx.saved_tensors
         fmt = torch.channels_last if ctx.nhwc else torch.contiguous_format
-        g = torch.ops.aten.threshold_backward(dy.to(x.dtype), y, 0).contiguous(memory_format=fmt)
+        dy = dy.to(x.dtype).contiguous(memory_format=fmt)
         n, c, h, w = x.shape
         dev = x.device
         dx = torch.empty_like(x)
@@ -252,10 +258,18 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
         db = torch.empty_like(bias)
         dpb = torch.empty_like(pre_bias) if pre_bias is not None else None
         ws = _bn_workspace(x, ctx.nhwc)
-        L.check(L.load().bb_bn_backward(_p(x), _p(g), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w, _p(pre_bias),
-                                        _p(weight), _p(bias), _p(mean), _p(invstd), 0, _p(ws), _p(dx), _p(dw),
-                                        _p(db), _p(dpb), _s(dev)),
-                "bb_bn_backward")
+        if RES_MASK:  # the ReLU's mask from the saved output inside the BatchNorm passes (threshold_backward)
+            g = torch.empty_like(x) if ctx.needs_input_grad[2] else None  # the residual's gradient
+            L.check(L.load().bb_bn_backward_res(_p(x), _p(dy), _p(y), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w,
+                                                _p(pre_bias), _p(weight), _p(bias), _p(mean), _p(invstd), _p(ws),
+                                                _p(dx), _p(dw), _p(db), _p(dpb), _p(g), _s(dev)),
+                    "bb_bn_backward_res")
+        else:
+            g = torch.ops.aten.threshold_backward(dy, y, 0).contiguous(memory_format=fmt)
+            L.check(L.load().bb_bn_backward(_p(x), _p(g), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w, _p(pre_bias),
+                                            _p(weight), _p(bias), _p(mean), _p(invstd), 0, _p(ws), _p(dx), _p(dw),
+                                            _p(db), _p(dpb), _s(dev)),
+                    "bb_bn_backward")
         gres = g
         if ctx.mailbox is not None and ctx.needs_input_grad[2]:
             ctx.mailbox.put(g)  # the block's first convolution adds it to its data gradient
@@ -572,11 +586,15 @@ class PPOLossFunction(torch.autograd.Function):
     """PPOAgent's minibatch loss (ppo.py:362-401) with the masked Categorical
     tail (network.py:173-180, 210-262) on bb_ppo_loss_forward/backward.
     Returns (total loss, stats[6] = policy / value / entropy / total loss,
-    approx_kl, clip_fraction); stats carry no gradient."""
+    approx_kl, clip_fraction); stats carry no gradient.  ``seed``: the tensor
+    the caller will backpropagate the loss with (its value read on the device
+    when the forward runs): forward and backward then run as one launch
+    (bb_ppo_loss_fused), and the backward hands those gradients over when
+    autograd passes that same tensor; any other gradient runs bb_ppo_loss_backward."""
 
     @staticmethod
     def forward(ctx, logits, values, masks, actions, old_log_probs, advantages, returns, clip: float,
-                value_coef: float, entropy_coef: float):
+                value_coef: float, entropy_coef: float, seed: Optional[torch.Tensor] = None):
         _need_cuda(logits, values, masks, actions, old_log_probs, advantages, returns)
         # bf16 logits and values (the autocast network's) are read as they are and get bf16 gradients
         # (bb_ppo_loss_*_bf16: the values of autograd's casts, without the cast launches)
@@ -589,14 +607,23 @@ class PPOLossFunction(torch.autograd.Function):
         dev = ins[0].device
         lib = L.load()
         ws = torch.empty((lib.bb_ppo_loss_workspace_bytes(b) + 7) // 8, dtype=torch.float64, device=dev)
+        cnt = _bgrad_counters(dev, 1)
         stats = torch.empty(6, dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        fn = lib.bb_ppo_loss_forward_bf16 if bf16 else lib.bb_ppo_loss_forward
-        L.check(fn(*[_p(t) for t in ins], b, float(clip), float(value_coef), float(entropy_coef), _p(ws), _p(stats),
-                   _p(loss), _s(dev)),
-                "bb_ppo_loss_forward")
+        coef = (float(clip), float(value_coef), float(entropy_coef))
+        ctx.seed, ctx.grads = None, None
+        if seed is not None and seed.is_cuda and seed.dtype == torch.float32 and seed.numel() == 1:
+            dlogits, dvalues = torch.empty_like(ins[0]), torch.empty_like(ins[1])
+            L.check(lib.bb_ppo_loss_fused(_p(ins[0]), _p(ins[1]), int(bf16), *[_p(t) for t in ins[2:]], b, *coef,
+                                          _p(seed), _p(dlogits), _p(dvalues), _p(ws), _p(cnt), _p(stats), _p(loss),
+                                          _s(dev)), "bb_ppo_loss_fused")
+            ctx.seed, ctx.grads = seed, (dlogits, dvalues)
+        else:
+            fn = lib.bb_ppo_loss_forward_bf16 if bf16 else lib.bb_ppo_loss_forward
+            L.check(fn(*[_p(t) for t in ins], b, *coef, _p(ws), _p(cnt), _p(stats), _p(loss), _s(dev)),
+                    "bb_ppo_loss_forward")
         ctx.save_for_backward(*ins)
-        ctx.coef = (float(clip), float(value_coef), float(entropy_coef))
+        ctx.coef = coef
         ctx.bf16 = bf16
         ctx.mark_non_differentiable(stats)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics
@@ -604,9 +631,13 @@ class PPOLossFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_loss, grad_stats):
-        ins = ctx.saved_tensors
         if grad_loss is None:
-            return (None,) * 10
+            return (None,) * 11
+        if ctx.grads is not None and grad_loss is ctx.seed:  # computed by the forward's launch
+            dlogits, dvalues = ctx.grads
+            ctx.grads = None
+            return dlogits, dvalues, None, None, None, None, None, None, None, None, None
+        ins = ctx.saved_tensors
         b = ins[0].shape[0]
         dev = ins[0].device
         g = grad_loss.float().reshape(1).contiguous()
@@ -615,7 +646,7 @@ class PPOLossFunction(torch.autograd.Function):
         fn = L.load().bb_ppo_loss_backward_bf16 if ctx.bf16 else L.load().bb_ppo_loss_backward
         L.check(fn(*[_p(t) for t in ins], b, *ctx.coef, _p(g), _p(dlogits), _p(dvalues), _s(dev)),
                 "bb_ppo_loss_backward")
-        return dlogits, dvalues, None, None, None, None, None, None, None, None
+        return dlogits, dvalues, None, None, None, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -785,6 +816,43 @@ class LinearBiasFunction(torch.autograd.Function):
         dx = gy.mm(weight) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(gy, x) if ctx.needs_input_grad[1] else None
         return dx, dw, db
+
+
+class LinearN1Function(torch.autograd.Function):
+    """F.linear(x, w, b) for a one-output bf16 Linear (the value head's last layer) on bb_linear_n1_forward /
+    _backward: one launch each way instead of torch's bias copy + GEMM and two GEMMs + a reduction."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        _need_cuda(x, weight)
+        rows, k = x.shape
+        y = torch.empty((rows, 1), dtype=x.dtype, device=x.device)
+        L.check(L.load().bb_linear_n1_forward(_p(x), _p(weight), _p(bias), rows, k, _p(y), _s(x.device)),
+                "bb_linear_n1_forward")
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        rows, k = x.shape
+        dev = x.device
+        lib = L.load()
+        gy = gy.contiguous()
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(weight)
+        db = torch.empty(1, dtype=x.dtype, device=dev) if ctx.has_bias else None
+        ws = torch.empty((lib.bb_linear_n1_workspace_bytes(rows, k) + 3) // 4, dtype=torch.float32, device=dev)
+        cnt = _bgrad_counters(dev, lib.bb_linear_n1_counters(k))
+        L.check(lib.bb_linear_n1_backward(_p(gy), _p(x), _p(weight), rows, k, _p(dx), _p(dw), _p(db), _p(ws), _p(cnt),
+                                          _s(dev)), "bb_linear_n1_backward")
+        return dx, dw, db
+
+
+def linear_n1_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    return (_bgrad_ok(x) and weight.dim() == 2 and weight.shape[0] == 1 and weight.shape[1] == x.shape[1]
+            and weight.dtype == torch.bfloat16 and weight.is_contiguous() and x.shape[1] % 8 == 0 and x.shape[0] > 0)
 
 
 class LinearCastFunction(torch.autograd.Function):

@@ -148,6 +148,8 @@ SIGNATURES = {
                                     _F, _P, _P, _P]),
     "bb_bn_backward": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                  _P]),
+    "bb_bn_backward_res": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                     _P, _P]),
     "bb_conv3x3_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
     "bb_conv3x3_prep": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "bb_conv3x3_prep_multi": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P]),
@@ -158,9 +160,10 @@ SIGNATURES = {
     "bb_conv3x3_f32_forward": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_linear_f32": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_ppo_loss_workspace_bytes": (C.c_int64, [_I32]),
-    "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
+    "bb_ppo_loss_forward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P, _P]),
     "bb_ppo_loss_backward": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
-    "bb_ppo_loss_forward_bf16": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
+    "bb_ppo_loss_forward_bf16": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P, _P]),
+    "bb_ppo_loss_fused": (C.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P]),
     "bb_ppo_loss_backward_bf16": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _F, _F, _F, _P, _P, _P, _P]),
     "bb_adam_clip_workspace_bytes": (C.c_int64, [_I32, _P]),
     "bb_adam_clip_step": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double, _F,
@@ -170,6 +173,10 @@ SIGNATURES = {
     "bb_conv_in_wgrad_workspace_bytes": (C.c_int64, [_I32]),
     "bb_conv_in_forward": (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     "bb_conv_in_wgrad": (C.c_int, [_P, _I32, _P, _I32, _P, _I32, _P, _P]),
+    "bb_linear_n1_workspace_bytes": (C.c_int64, [_I32, _I32]),
+    "bb_linear_n1_counters": (C.c_int32, [_I32]),
+    "bb_linear_n1_forward": (C.c_int, [_P, _P, _P, _I32, _I32, _P, _P]),
+    "bb_linear_n1_backward": (C.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "bb_linear_wgrad_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
     "bb_linear_wgrad_counters": (C.c_int32, [_I32, _I32]),
     "bb_linear_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),

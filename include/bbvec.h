@@ -38,7 +38,9 @@ extern "C" {
                               6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
                                  bb_conv3x3_f32_prep / _forward, bb_linear_f32;
                               7: bb_ppo_loss_forward_bf16 / _backward_bf16;
-                              8: bb_dropout_forward, bb_linear_bgrad, bb_linear_wgrad; bb_conv_in_forward / _wgrad */
+                              8: bb_dropout_forward, bb_linear_bgrad, bb_linear_wgrad, bb_linear_n1_*;
+                                 bb_conv_in_forward / _wgrad; bb_bn_backward_res; bb_ppo_loss_fused and the
+                                 loss forward's d_cnt (one launch, the statistics finalised in it) */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -316,8 +318,8 @@ int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32_t N, int32
  * where round is the activation dtype's rounding (the BatchNorm output tensor
  * of the unfused module) and the sum is rounded once, as torch's add.  d_res
  * has x's shape, dtype and layout (16-byte aligned).  The backward is
- * bb_bn_backward with relu = 0 over dy masked by y > 0 (the caller's
- * threshold_backward), whose masked dy is also the residual's gradient. */
+ * bb_bn_backward_res (dy masked by y > 0, as threshold_backward; the masked dy
+ * is also the residual's gradient). */
 int bb_bn_forward_res(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N,
                       int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                       const float* d_bias, float eps, int32_t relu, double* d_ws, float* d_save_mean,
@@ -328,6 +330,14 @@ int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhw
                    const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
                    int32_t relu, double* d_ws, void* d_dx, float* d_dweight, float* d_dbias,
                    float* d_dpre_bias, void* stream);
+/* The backward of bb_bn_forward_res with its ReLU: bb_bn_backward (relu = 0) over g = (y > 0 ? dy : 0), y the
+ * forward's output (torch's threshold_backward), the mask applied inside the reduction and elementwise
+ * passes instead of a pass of its own; g, the residual's gradient, is written to d_gres when non-NULL
+ * (x's shape, dtype and layout).  Three launches, as bb_bn_backward. */
+int bb_bn_backward_res(const void* d_x, const void* d_dy, const void* d_y, int32_t dtype, int32_t nhwc, int32_t N,
+                       int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias,
+                       const float* d_save_mean, const float* d_save_invstd, double* d_ws, void* d_dx,
+                       float* d_dweight, float* d_dbias, float* d_dpre_bias, void* d_gres, void* stream);
 
 /* The PPO minibatch loss (PPOAgent.update, ppo.py:362-401) with the masked
  * Categorical tail (network.py:173-180, 210-262), fused, forward and backward.
@@ -335,15 +345,21 @@ int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhw
  * (non-zero = legal), action, old log-prob, advantage, return and value.
  * Forward writes d_stats[6] = {policy_loss, value_loss, entropy, total_loss,
  * approx_kl, clip_fraction} (the reference's update metrics) and, if non-NULL,
- * d_loss[0] = total_loss; d_ws is scratch of bb_ppo_loss_workspace_bytes(B)
- * bytes.  Backward takes d(total_loss) from d_grad_loss[0] (device memory, so
- * a HIP graph can replay it) and writes d/dlogits [B][192] and d/dvalues [B],
- * following torch autograd's rules for min / clamp / log. */
+ * d_loss[0] = total_loss, in one launch: d_ws is scratch of
+ * bb_ppo_loss_workspace_bytes(B) bytes for the blocks' partial sums, which the
+ * last block to finish adds in a fixed order (deterministic); d_cnt is one
+ * uint32 counter, zero before the first launch and re-armed by each (ABI 8;
+ * one counter per stream).  Backward takes d(total_loss) from d_grad_loss[0]
+ * (device memory, so a HIP graph can replay it) and writes d/dlogits [B][192]
+ * and d/dvalues [B], following torch autograd's rules for min / clamp / log.
+ * bb_ppo_loss_fused is both in one launch (the caller knows the loss gradient
+ * before the forward: the root of its backward), f32 (bf16 = 0) or bf16 (1)
+ * logits / values and gradients. */
 int64_t bb_ppo_loss_workspace_bytes(int32_t B);
 int bb_ppo_loss_forward(const float* d_logits, const float* d_values, const float* d_mask,
                         const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
                         const float* d_ret, int32_t B, float clip, float value_coef,
-                        float entropy_coef, double* d_ws, float* d_stats, float* d_loss,
+                        float entropy_coef, double* d_ws, uint32_t* d_cnt, float* d_stats, float* d_loss,
                         void* stream);
 int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const float* d_mask,
                          const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
@@ -356,11 +372,16 @@ int bb_ppo_loss_backward(const float* d_logits, const float* d_values, const flo
 int bb_ppo_loss_forward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
                              const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
                              const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
-                             double* d_ws, float* d_stats, float* d_loss, void* stream);
+                             double* d_ws, uint32_t* d_cnt, float* d_stats, float* d_loss, void* stream);
 int bb_ppo_loss_backward_bf16(const void* d_logits, const void* d_values, const float* d_mask,
                               const int64_t* d_actions, const float* d_old_logp, const float* d_adv,
                               const float* d_ret, int32_t B, float clip, float value_coef, float entropy_coef,
                               const float* d_grad_loss, void* d_dlogits, void* d_dvalues, void* stream);
+int bb_ppo_loss_fused(const void* d_logits, const void* d_values, int32_t bf16, const float* d_mask,
+                      const int64_t* d_actions, const float* d_old_logp, const float* d_adv, const float* d_ret,
+                      int32_t B, float clip, float value_coef, float entropy_coef, const float* d_grad_loss,
+                      void* d_dlogits, void* d_dvalues, double* d_ws, uint32_t* d_cnt, float* d_stats, float* d_loss,
+                      void* stream);
 
 /* The CNN's 3x3 / padding-1 convolutions over 8x8 boards (network.py:75-117,
  * ResidualBlock network.py:14-30; nn.Conv2d.forward and its autograd
@@ -482,6 +503,18 @@ int bb_conv_in_wgrad(const float* d_x, int32_t x_nhwc, const void* d_dy, int32_t
  * (bb_linear_wgrad_workspace_bytes(rows, N, K) bytes) and the last split of a tile adds them; d_cnt: the
  * bb_linear_wgrad_counters(N, K) uint32 counters, zero before and after each launch (as bb_linear_bgrad's,
  * and the same counter block may serve both on one stream). */
+/* bb_linear_n1_forward / _backward: a bf16 Linear with one output (the value head's Linear(128, 1)), x bf16
+ * [rows][K], w bf16 [K], b bf16 [1] (NULL: none), K a multiple of 8, 16-byte aligned.  Forward: y[r] =
+ * bf16(sum_k x[r][k] w[k] + b), f32 sums.  Backward: dx[r][k] = bf16(gy[r] w[k]), dW[k] = sum_r gy[r] x[r][k],
+ * db = sum_r gy[r] (d_db NULL: skipped), f32 sums in a fixed order rounded to bf16; row chunks publish
+ * partials to d_ws (bb_linear_n1_workspace_bytes(rows, K) bytes) with bb_linear_n1_counters(K) zeroed
+ * counters in d_cnt (as bb_linear_bgrad).  One launch each. */
+int64_t bb_linear_n1_workspace_bytes(int32_t rows, int32_t K);
+int32_t bb_linear_n1_counters(int32_t K);
+int bb_linear_n1_forward(const void* d_x, const void* d_w, const void* d_b, int32_t rows, int32_t K, void* d_y,
+                         void* stream);
+int bb_linear_n1_backward(const void* d_gy, const void* d_x, const void* d_w, int32_t rows, int32_t K, void* d_dx,
+                          void* d_dw, void* d_db, float* d_ws, uint32_t* d_cnt, void* stream);
 int64_t bb_linear_wgrad_workspace_bytes(int32_t rows, int32_t N, int32_t K);
 int32_t bb_linear_wgrad_counters(int32_t N, int32_t K);
 int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, int32_t N, int32_t K, void* d_dw, float* d_ws,

@@ -153,11 +153,15 @@ def test_network_fused_casts_equal_autocast(cuda, monkeypatch):
             assert torch.allclose(gr, res[False][2][n], rtol=1e-2, atol=1e-4), n
 
 
+@pytest.mark.parametrize("res_mask", [False, True])
 @pytest.mark.parametrize("dtype,nhwc", [(torch.float32, False), (torch.float32, True), (torch.bfloat16, True)])
-def test_bn_add_relu_equals_composite(cuda, dtype, nhwc):
+def test_bn_add_relu_equals_composite(cuda, dtype, nhwc, res_mask, monkeypatch):
     """BatchNormAddReLUFunction == BatchNormReLUFunction(relu=False) -> + res ->
-    relu, forward, running statistics and every gradient, bit for bit."""
+    relu, forward, running statistics and every gradient, bit for bit; the backward both ways
+    (threshold_backward + bb_bn_backward, and bb_bn_backward_res with the mask inside the passes)."""
     from runtime import kernels as K
+
+    monkeypatch.setattr(K, "RES_MASK", res_mask)
 
     g = torch.Generator(device=cuda).manual_seed(11)
     fmt = torch.channels_last if nhwc else torch.contiguous_format

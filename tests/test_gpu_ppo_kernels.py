@@ -313,3 +313,38 @@ def test_fused_ppo_loss_bf16_inputs_equal_cast_path(cuda, density):
         res.append((loss.detach(), stats, lg.grad, vg.grad))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_fused_ppo_loss_one_launch_equals_two(cuda, bf16):
+    """bb_ppo_loss_fused (forward and backward in one launch, the loss gradient given up front as the seed that
+    PPOAgent backpropagates with) == bb_ppo_loss_forward + bb_ppo_loss_backward, bit for bit: loss, metrics and
+    both gradients; a seed of 0.5 halves the gradients exactly; a backward with another gradient tensor than the
+    seed runs the backward kernel; odd batch sizes (the in-kernel finalisation's last block)."""
+    from agents.ppo import PPOConfig
+    from runtime.kernels import PPOLossFunction
+
+    cfg = PPOConfig()
+    for B in (2048, 37, 1):
+        torch.manual_seed(B)
+        dt = torch.bfloat16 if bf16 else torch.float32
+        lb = (torch.randn(B, 192, device=cuda) * 3).to(dt)
+        vb = torch.randn(B, device=cuda).to(dt)
+        mask = (torch.rand(B, 192, device=cuda) < 0.3).float()
+        mask[torch.arange(B, device=cuda), torch.randint(0, 192, (B,), device=cuda)] = 1.0
+        actions = torch.multinomial(mask, 1).squeeze(1)
+        old = -torch.rand(B, device=cuda) * 4
+        adv, ret = torch.randn(B, device=cuda), torch.randn(B, device=cuda)
+        args = (mask, actions, old, adv, ret, cfg.clip_epsilon, cfg.value_coef, cfg.entropy_coef)
+        out = {}
+        for mode in ("two", "fused", "half", "other"):
+            lg, vg = lb.clone().requires_grad_(True), vb.clone().requires_grad_(True)
+            seed = torch.full((), 0.5 if mode == "half" else 1.0, device=cuda)
+            loss, stats = PPOLossFunction.apply(lg, vg, *args, None if mode == "two" else seed)
+            loss.backward(torch.ones((), device=cuda) if mode == "other" else (seed if mode != "two" else None))
+            out[mode] = (loss.detach(), stats.clone(), lg.grad.clone(), vg.grad.clone())
+        for m in ("fused", "other"):
+            for a, b in zip(out["two"], out[m]):
+                assert torch.equal(a, b), (B, m)
+        assert torch.equal(out["half"][2].float(), (out["two"][2].float() * 0.5).to(dt).float())
+        assert torch.equal(out["half"][3].float(), (out["two"][3].float() * 0.5).to(dt).float())
