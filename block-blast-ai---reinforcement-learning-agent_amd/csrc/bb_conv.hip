@@ -33,6 +33,7 @@ namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -816,7 +817,14 @@ hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, flo
 // transposed through LDS; a workgroup's partial [t][co][ci] goes to conv_wgrad_reduce (fixed chunk order).
 // ---------------------------------------------------------------------------
 constexpr int kInCout = 64, kInK = 36, kInWaves = 4;
-constexpr int kInWgChunks = 128;  // weight-gradient workgroups (partials) at most
+#ifndef BB_IN_WG_CHUNKS
+#define BB_IN_WG_CHUNKS 128
+#endif
+#ifndef BB_IN_FWD_BLOCKS
+#define BB_IN_FWD_BLOCKS 256
+#endif
+constexpr int kInWgChunks = BB_IN_WG_CHUNKS;  // weight-gradient workgroups (partials) at most
+constexpr int kInFwdBlocks = BB_IN_FWD_BLOCKS;  // forward workgroups at most (4 boards each per pass)
 
 __device__ __forceinline__ bf16x8 pack8(float4 a, float4 b) {
   bf16x8 r;
@@ -825,49 +833,51 @@ __device__ __forceinline__ bf16x8 pack8(float4 a, float4 b) {
   return r;
 }
 
-// board b of x -> the wave's zero-haloed [10][10] pixel image of float4 (4 input channels)
-__device__ __forceinline__ void in_load_board(const float* __restrict__ x, int x_nhwc, int b, int lane,
-                                              float4* xpad) {
-  const float4 v = reinterpret_cast<const float4*>(x + (size_t)b * 256)[lane];
-  if (x_nhwc) {  // lane = pixel
-    xpad[((lane >> 3) + 1) * 10 + (lane & 7) + 1] = v;
-  } else {  // lane: channel lane >> 4, pixels 4 (lane & 15) .. + 3
-    const int ci = lane >> 4, p0 = (lane & 15) * 4, r = p0 >> 3, c0 = p0 & 7;
-    float* f = reinterpret_cast<float*>(xpad) + ((r + 1) * 10 + c0 + 1) * 4 + ci;
-    f[0] = v.x;
-    f[4] = v.y;
-    f[8] = v.z;
-    f[12] = v.w;
-  }
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// one lane's A fragments of the input-layer weights: A[co = 16 mt + l16][k = 32 s + 8 g + j], k = 4 t + ci,
+// straight from the f32 weight (L2-resident; 16-byte loads for a channels_last weight), rounded to bf16
+__device__ __forceinline__ float4 in_weight_taps(const float* __restrict__ w, int wl, int co, int t) {
+  if (t >= 9) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if (wl) return *reinterpret_cast<const float4*>(w + (co * 9 + t) * 4);
+  return make_float4(w[(co * 4) * 9 + t], w[(co * 4 + 1) * 9 + t], w[(co * 4 + 2) * 9 + t], w[(co * 4 + 3) * 9 + t]);
 }
 
-__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void in_weight_frags(const float* __restrict__ w, int wl, int g, int l16, bf16x8 afr[4][2]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int co = 16 * mt + l16, t = 8 * s2 + 2 * g;
+      afr[mt][s2] = pack8(in_weight_taps(w, wl, co, t), in_weight_taps(w, wl, co, t + 1));
+    }
+}
 
 __global__ void __launch_bounds__(256) conv_in_fwd_kernel(const float* __restrict__ x, int x_nhwc,
                                                           const float* __restrict__ w, int wl, int nb,
                                                           uint16_t* __restrict__ y) {
-  __shared__ float wsh[kInCout * kInK];      // [co][k]
   __shared__ float4 xpad[kInWaves][100];      // per wave: [(r + 1) * 10 + c + 1] -> 4 channels
   __shared__ uint4 ost[kInWaves][64 * 8];     // per wave: [pixel][16-B chunk ^ (pixel & 7)] of 8 channels
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
-  for (int i = threadIdx.x; i < kInCout * kInK; i += 256) {
-    const int co = i / kInK, k = i % kInK, t = k >> 2, ci = k & 3;
-    wsh[i] = w[wl ? (co * 9 + t) * 4 + ci : (co * 4 + ci) * 9 + t];
-  }
+  const int stride = gridDim.x * kInWaves;
+  int b = blockIdx.x * kInWaves + wave;
+  // the first board's load in flight with the weight fragments' (every wave works alone: no barrier)
+  float4 xv = b < nb ? reinterpret_cast<const float4*>(x + (size_t)b * 256)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int i = lane; i < 100; i += 64) xpad[wave][i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-  bf16x8 afr[4][2];  // A[co = 16 mt + l16][k = 32 s + 8 g + j]
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 32 * s2 + 8 * g + j;
-        afr[mt][s2][j] = (short)(k < kInK ? f2bf(wsh[(16 * mt + l16) * kInK + k]) : 0);
-      }
-  for (int b = blockIdx.x * kInWaves + wave; b < nb; b += gridDim.x * kInWaves) {
-    in_load_board(x, x_nhwc, b, lane, xpad[wave]);
+  bf16x8 afr[4][2];
+  in_weight_frags(w, wl, g, l16, afr);
+  for (; b < nb; b += stride) {
+    if (x_nhwc) {  // lane = pixel
+      xpad[wave][((lane >> 3) + 1) * 10 + (lane & 7) + 1] = xv;
+    } else {  // lane: channel lane >> 4, pixels 4 (lane & 15) .. + 3
+      const int ci = lane >> 4, p0 = (lane & 15) * 4, r = p0 >> 3, c0 = p0 & 7;
+      float* f = reinterpret_cast<float*>(xpad[wave]) + ((r + 1) * 10 + c0 + 1) * 4 + ci;
+      f[0] = xv.x;
+      f[4] = xv.y;
+      f[8] = xv.z;
+      f[12] = xv.w;
+    }
+    if (b + stride < nb) xv = reinterpret_cast<const float4*>(x + (size_t)(b + stride) * 256)[lane];  // next board
     lds_wait();
     f32x4 acc[4][4];
 #pragma unroll
@@ -880,9 +890,12 @@ __global__ void __launch_bounds__(256) conv_in_fwd_kernel(const float* __restric
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int t0 = 8 * s2 + 2 * g;  // taps t0, t0 + 1 (k = 4 t + ci)
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 v0 = t0 < 9 ? xpad[wave][(r + t0 / 3) * 10 + c + t0 % 3] : z;
-        const float4 v1 = t0 + 1 < 9 ? xpad[wave][(r + (t0 + 1) / 3) * 10 + c + (t0 + 1) % 3] : z;
+        // loads at clamped taps, then a value select (a select of addresses becomes a flat load from LDS or stack)
+        const int ta = min(t0, 8), tb = min(t0 + 1, 8);
+        float4 v0 = xpad[wave][(r + ta / 3) * 10 + c + ta % 3];
+        float4 v1 = xpad[wave][(r + tb / 3) * 10 + c + tb % 3];
+        if (t0 >= 9) v0 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t0 + 1 >= 9) v1 = make_float4(0.f, 0.f, 0.f, 0.f);
         const bf16x8 bfr = pack8(v0, v1);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -910,46 +923,71 @@ __global__ void __launch_bounds__(256) conv_in_fwd_kernel(const float* __restric
   }
 }
 
+__device__ __forceinline__ s16x4 in_tr_read(const uint16_t* lds) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)lds);
+}
+
 __global__ void __launch_bounds__(256) conv_in_wgrad_kernel(const float* __restrict__ x, int x_nhwc,
                                                             const uint16_t* __restrict__ dy, int nb,
                                                             float* __restrict__ part) {
-  // per wave: dyT [64 co][64 pixels] bf16 (16-B chunk of 8 pixels at chunk ^ ((co >> 3) & 7)), then the padded
+  // per wave: dy [64 pixels][64 co] bf16 as stored (read k-major by ds_read_b64_tr_b16), then the padded
   // board; after the board loop the same bytes hold waves 1-3's sums for wave 0 to add
-  constexpr int kDyT = 64 * 64 * 2, kXp = 100 * 16, kPerWave = kDyT + kXp;
+  constexpr int kDy = 64 * 64 * 2, kXp = 100 * 16, kPerWave = kDy + kXp;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kInWaves * kPerWave];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
-  uint16_t* dyt = reinterpret_cast<uint16_t*>(smem + wave * kPerWave);
-  float4* xpad = reinterpret_cast<float4*>(smem + wave * kPerWave + kDyT);
+  const int q4 = l16 >> 2, p4 = l16 & 3;  // this lane's row / column group in a transposed read
+  uint16_t* dys = reinterpret_cast<uint16_t*>(smem + wave * kPerWave);
+  float4* xpad = reinterpret_cast<float4*>(smem + wave * kPerWave + kDy);
   for (int i = lane; i < 100; i += 64) xpad[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   f32x4 acc[4][3];  // C[co = 16 mt + 4 g + i][k = 16 nt + l16]
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int b = blockIdx.x * kInWaves + wave; b < nb; b += gridDim.x * kInWaves) {
-    const uint4* db = reinterpret_cast<const uint4*>(dy + (size_t)b * 64 * kInCout);
-    uint4 dv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dv[q] = db[lane + 64 * q];
-    in_load_board(x, x_nhwc, b, lane, xpad);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {  // pixel p, channels 8 ch .. 8 ch + 7 -> dyT[co][p]
-      const int idx = lane + 64 * q, p = idx >> 3, ch = idx & 7;
-      const uint32_t wv[4] = {dv[q].x, dv[q].y, dv[q].z, dv[q].w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int co = 8 * ch + e;
-        dyt[co * 64 + (((p >> 3) ^ ch) << 3) + (p & 7)] = (uint16_t)(e & 1 ? wv[e >> 1] >> 16 : wv[e >> 1]);
-      }
+  const int stride = gridDim.x * kInWaves;
+  int b = blockIdx.x * kInWaves + wave;
+  // board bb's dy (8 x 16 B per lane) and x (16 B) into registers
+#define BB_IN_FETCH(bb)                                                              \
+  {                                                                                  \
+    const uint4* db_ = reinterpret_cast<const uint4*>(dy + (size_t)(bb) * 64 * kInCout); \
+    dv0 = db_[lane];                                                                 \
+    dv1 = db_[lane + 64];                                                            \
+    dv2 = db_[lane + 128];                                                           \
+    dv3 = db_[lane + 192];                                                           \
+    dv4 = db_[lane + 256];                                                           \
+    dv5 = db_[lane + 320];                                                           \
+    dv6 = db_[lane + 384];                                                           \
+    dv7 = db_[lane + 448];                                                           \
+    xv = reinterpret_cast<const float4*>(x + (size_t)(bb) * 256)[lane];              \
+  }
+  uint4 dv0, dv1, dv2, dv3, dv4, dv5, dv6, dv7;
+  float4 xv;
+  if (b < nb) BB_IN_FETCH(b)
+  for (; b < nb; b += stride) {
+    {  // [pixel][co], as in HBM
+      uint4* d_ = reinterpret_cast<uint4*>(dys) + lane;
+      d_[0] = dv0, d_[64] = dv1, d_[128] = dv2, d_[192] = dv3, d_[256] = dv4, d_[320] = dv5, d_[384] = dv6, d_[448] = dv7;
     }
+    if (x_nhwc) {
+      xpad[((lane >> 3) + 1) * 10 + (lane & 7) + 1] = xv;
+    } else {
+      const int ci = lane >> 4, p0 = (lane & 15) * 4, r = p0 >> 3, c0 = p0 & 7;
+      float* f = reinterpret_cast<float*>(xpad) + ((r + 1) * 10 + c0 + 1) * 4 + ci;
+      f[0] = xv.x;
+      f[4] = xv.y;
+      f[8] = xv.z;
+      f[12] = xv.w;
+    }
+    if (b + stride < nb) BB_IN_FETCH(b + stride)  // the next board's loads in flight during this one
     lds_wait();
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 afr[4];  // A[co = 16 mt + l16][pixel = 32 s + 8 g + j]
+      bf16x8 afr[4];  // A[co = 16 mt + l16][pixel = 32 s + 8 g + j]: two 4-pixel transposed reads
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const int co = 16 * mt + l16;
-        afr[mt] = *reinterpret_cast<const bf16x8*>(dyt + co * 64 + (((4 * s2 + g) ^ ((co >> 3) & 7)) << 3));
+        const s16x4 lo = in_tr_read(dys + (32 * s2 + 8 * g + q4) * 64 + 16 * mt + 4 * p4);
+        const s16x4 hi = in_tr_read(dys + (32 * s2 + 8 * g + 4 + q4) * 64 + 16 * mt + 4 * p4);
+        afr[mt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int nt = 0; nt < 3; ++nt) {
@@ -965,6 +1003,7 @@ __global__ void __launch_bounds__(256) conv_in_wgrad_kernel(const float* __restr
       }
     }
   }
+#undef BB_IN_FETCH
   __syncthreads();  // every wave is done with its LDS images
   float* red = reinterpret_cast<float*>(smem);  // [3][9][64][4]: waves 1-3
   constexpr int kW = 9 * kInCout * 4;
@@ -1061,7 +1100,7 @@ hipError_t launch_conv_in_forward(const float* x, int x_nhwc, const float* w, in
   if (nb <= 0 || !x || !w || !y || (wl != 0 && wl != 1) || (reinterpret_cast<uintptr_t>(x) & 15) ||
       (reinterpret_cast<uintptr_t>(y) & 15))
     return hipErrorInvalidValue;
-  const int blocks = std::min((nb + kInWaves - 1) / kInWaves, 4096);
+  const int blocks = std::min((nb + kInWaves - 1) / kInWaves, kInFwdBlocks);
   hipLaunchKernelGGL(conv_in_fwd_kernel, dim3(blocks), dim3(256), 0, s, x, x_nhwc ? 1 : 0, w, wl, nb, (uint16_t*)y);
   return hipGetLastError();
 }

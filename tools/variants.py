@@ -104,6 +104,13 @@ VARIANTS = {
     "drop256": ["-DBB_DROP_BLOCKS=256"],
     "drop512": ["-DBB_DROP_BLOCKS=512"],
     "dropu1": ["-DBB_DROP_UNROLL=1"],
+    # the input layer (conv 4 -> 64): forward workgroups at most (shipped 256: two boards per wave at 2,048
+    # boards), weight-gradient partial chunks (shipped 128); tools/bench_conv_in.py, profiles/r05/ci/
+    "if128": ["-DBB_IN_FWD_BLOCKS=128"],
+    "if512": ["-DBB_IN_FWD_BLOCKS=512"],
+    "iw32": ["-DBB_IN_WG_CHUNKS=32"],
+    "iw64": ["-DBB_IN_WG_CHUNKS=64"],
+    "iw256": ["-DBB_IN_WG_CHUNKS=256"],
 }
 
 
