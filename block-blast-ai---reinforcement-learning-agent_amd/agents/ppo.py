@@ -603,7 +603,10 @@ class PPOAgent(BaseAgent):
             self._remove_dp_hooks()
             for p in self.network.parameters():
                 p.grad = None
-            with K.deferred_wgrad(self.device):  # conv weight gradients beside the rest of the backward
+            # conv weight gradients beside the rest of the backward (opt-in), or their partial-sum reductions
+            # carried by the next BatchNorm backward's launch (every .grad is None here, so autograd keeps the
+            # returned tensors and nothing reads them before the block closes)
+            with K.deferred_wgrad(self.device), K.wgrad_piggyback(self.device):
                 self._backward_loss(loss)
         self._clip_and_step()
 

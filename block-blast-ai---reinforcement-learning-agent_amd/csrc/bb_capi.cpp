@@ -704,6 +704,27 @@ extern "C" int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, 
   return BB_OK;
 }
 
+extern "C" int bb_bn_backward_red(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N, int32_t C,
+                                  int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias,
+                                  const float* d_save_mean, const float* d_save_invstd, int32_t relu, double* d_ws,
+                                  void* d_dx, float* d_dweight, float* d_dbias, float* d_dpre_bias,
+                                  const float* d_conv_ws, int32_t conv_chunks, int32_t conv_cin, int32_t conv_cout,
+                                  int32_t conv_w_layout, float* d_conv_dw, void* stream) {
+  int rc = bn_check(dtype, nhwc, N, C, HW);
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_dy || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx || !d_conv_ws ||
+      !d_conv_dw || conv_chunks <= 0 || (conv_w_layout != 0 && conv_w_layout != 1) ||
+      !conv3x3_supported(conv_cin, conv_cout))
+    return fail(nullptr, BB_ERR_ARG, "bb_bn_backward_red: bad arguments");
+  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
+  const WgradReduceJob job{d_conv_ws, conv_chunks, conv_cout, conv_cin, conv_w_layout, d_conv_dw};
+  hipError_t st = launch_bn_backward(d_x, d_dy, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, d_save_mean,
+                                     d_save_invstd, relu, d_ws, d_dx, d_dweight, d_dbias, d_dpre_bias,
+                                     (hipStream_t)stream, nullptr, nullptr, &job);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_backward_red");
+  return BB_OK;
+}
+
 extern "C" int bb_bn_backward_res(const void* d_x, const void* d_dy, const void* d_y, int32_t dtype, int32_t nhwc,
                                   int32_t N, int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                                   const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
@@ -885,6 +906,34 @@ extern "C" int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, in
   if (!al16(d_x) || !al16(d_dy)) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_wgrad: tensors must be 16-byte aligned");
   hipError_t st = launch_conv3x3_wgrad(d_x, d_dy, N, cin, cout, d_ws, w_layout, d_dw, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_wgrad");
+  return BB_OK;
+}
+
+extern "C" int32_t bb_conv3x3_wgrad_chunks(int32_t N, int32_t cin, int32_t cout) {
+  if (conv_check(N, cin, cout, "bb_conv3x3_wgrad_chunks") != BB_OK) return -1;
+  return conv3x3_wgrad_chunks_used(N, cin, cout);
+}
+
+extern "C" int bb_conv3x3_wgrad_partial(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout,
+                                        float* d_ws, void* stream) {
+  int rc = conv_check(N, cin, cout, "bb_conv3x3_wgrad_partial");
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_dy || !d_ws) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_wgrad_partial: NULL argument");
+  if (!al16(d_x) || !al16(d_dy))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_wgrad_partial: tensors must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_wgrad_partial(d_x, d_dy, N, cin, cout, d_ws, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_wgrad_partial");
+  return BB_OK;
+}
+
+extern "C" int bb_conv3x3_wgrad_reduce(const float* d_ws, int32_t chunks, int32_t cin, int32_t cout, int32_t w_layout,
+                                       float* d_dw, void* stream) {
+  int rc = conv_check(1, cin, cout, "bb_conv3x3_wgrad_reduce");
+  if (rc != BB_OK) return rc;
+  if (!d_ws || !d_dw || chunks <= 0 || (w_layout != 0 && w_layout != 1))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_wgrad_reduce: bad arguments");
+  hipError_t st = launch_conv3x3_wgrad_reduce(d_ws, chunks, cin, cout, w_layout, d_dw, (hipStream_t)stream);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_wgrad_reduce");
   return BB_OK;
 }
 

@@ -791,20 +791,32 @@ hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, c
   return hipGetLastError();
 }
 
+int wgrad_used(int nb, int cin, int cout) {  // chunks that hold boards
+  const int bpc = wgrad_bpc(nb, wgrad_chunks(nb, cin, cout));
+  return (nb + bpc - 1) / bpc;
+}
+
 template <int CIN, int COUT>
-hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s) {
-  const int nchunk = wgrad_chunks(nb, CIN, COUT);
-  const int bpc = wgrad_bpc(nb, nchunk);
-  const int used = (nb + bpc - 1) / bpc;  // chunks that hold boards
-  const int used8 = (used + 7) / 8 * 8;
+hipError_t wgrad_partial_t(const void* x, const void* dy, int nb, float* ws, hipStream_t s) {
+  const int bpc = wgrad_bpc(nb, wgrad_chunks(nb, CIN, COUT));
+  const int used8 = (wgrad_used(nb, CIN, COUT) + 7) / 8 * 8;
   hipLaunchKernelGGL((conv_wgrad_kernel<CIN, COUT>), dim3((CIN / kWgTile) * (COUT / kWgTile) * used8), dim3(kWgThreads),
                      0, s, (const uint16_t*)x, (const uint16_t*)dy, ws, nb, bpc);
-  hipError_t st = hipGetLastError();
-  if (st != hipSuccess) return st;
-  const int n = 9 * COUT * CIN;
-  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ws, used, COUT,
-                     CIN, wl, dw);
   return hipGetLastError();
+}
+
+hipError_t wgrad_reduce(const float* ws, int used, int cin, int cout, int wl, float* dw, hipStream_t s) {
+  const int n = 9 * cout * cin;
+  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, s, ws, used, cout, cin,
+                     wl, dw);
+  return hipGetLastError();
+}
+
+template <int CIN, int COUT>
+hipError_t wgrad_t(const void* x, const void* dy, int nb, float* ws, int wl, float* dw, hipStream_t s) {
+  hipError_t st = wgrad_partial_t<CIN, COUT>(x, dy, nb, ws, s);
+  if (st != hipSuccess) return st;
+  return wgrad_reduce(ws, wgrad_used(nb, CIN, COUT), CIN, COUT, wl, dw, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1082,6 +1094,20 @@ hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin,
   if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd);
   if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd);
   return fwd_t<128, 128>(x, w, nb, y, s, radd);
+}
+
+int conv3x3_wgrad_chunks_used(int nb, int cin, int cout) { return wgrad_used(nb, cin, cout); }
+
+hipError_t launch_conv3x3_wgrad_partial(const void* x, const void* dy, int nb, int cin, int cout, float* ws,
+                                        hipStream_t s) {
+  if (cin == 64 && cout == 64) return wgrad_partial_t<64, 64>(x, dy, nb, ws, s);
+  if (cin == 64 && cout == 128) return wgrad_partial_t<64, 128>(x, dy, nb, ws, s);
+  if (cin == 128 && cout == 64) return wgrad_partial_t<128, 64>(x, dy, nb, ws, s);
+  return wgrad_partial_t<128, 128>(x, dy, nb, ws, s);
+}
+
+hipError_t launch_conv3x3_wgrad_reduce(const float* ws, int used, int cin, int cout, int wl, float* dw, hipStream_t s) {
+  return wgrad_reduce(ws, used, cin, cout, wl, dw, s);
 }
 
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,

@@ -107,10 +107,17 @@ hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc
                              const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
                              float* save_mean, float* save_invstd, float* rmean, float* rvar, float momentum,
                              int64_t* nbt, void* y, hipStream_t s);
+// a board convolution's weight-gradient partial-sum reduction (csrc/bb_conv.hip conv_wgrad_reduce's arguments),
+// run inside a BatchNorm backward finalisation's launch by bb_bn_backward_red
+struct WgradReduceJob {  // conv_wgrad_reduce's arguments
+  const float* part;
+  int nchunk, cout, cin, wl;
+  float* dw;
+};
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
                               int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s,
-                              const void* mask = nullptr, void* gout = nullptr);
+                              const void* mask = nullptr, void* gout = nullptr, const WgradReduceJob* job = nullptr);
 
 bool conv3x3_supported(int cin, int cout);
 int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout);
@@ -121,6 +128,12 @@ hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin,
                                   const void* radd = nullptr);
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);
+// the weight gradient in two parts: the partial-sum kernel, and the fixed-order sum of its `used` chunks (which
+// bb_bn_backward_red can run inside the next BatchNorm finalisation's launch)
+int conv3x3_wgrad_chunks_used(int nb, int cin, int cout);
+hipError_t launch_conv3x3_wgrad_partial(const void* x, const void* dy, int nb, int cin, int cout, float* ws,
+                                        hipStream_t s);
+hipError_t launch_conv3x3_wgrad_reduce(const float* ws, int used, int cin, int cout, int wl, float* dw, hipStream_t s);
 
 // the input layer, conv 4 -> 64 (x f32 NCHW or NHWC, w f32 [64][4][3][3] wl 0 or [64][3][3][4] wl 1)
 int64_t conv_in_wgrad_workspace_bytes(int nb);

@@ -253,6 +253,25 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
   }
 }
 
+// A board convolution's weight-gradient partial sums, added in chunk order (csrc/bb_conv.hip
+// conv_wgrad_reduce's arithmetic, bit for bit): dw[co][ci][t] (wl 0) or dw[co][t][ci] (wl 1).
+__device__ __forceinline__ void wgrad_reduce_at(const WgradReduceJob& j, int i) {
+  const int n = 9 * j.cout * j.cin;
+  if (i >= n) return;
+  float s = 0.f;
+  int c = 0;
+  for (; c + 16 <= j.nchunk; c += 16) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = j.part[(size_t)(c + k) * n + i];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += v[k];
+  }
+  for (; c < j.nchunk; ++c) s += j.part[(size_t)c * n + i];
+  const int ci = i % j.cin, co = (i / j.cin) % j.cout, t = i / (j.cin * j.cout);
+  j.dw[j.wl ? (co * 9 + t) * j.cin + ci : (co * j.cin + ci) * 9 + t] = s;
+}
+
 // Per-channel coefficients of the elementwise passes, packed 8 floats per
 // channel so an apply thread loads them as two 16-byte vectors:
 //   forward  {pre_bias, mean, invstd * weight, bias, -, -, -, -}
@@ -318,13 +337,20 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_fwd(const double* __re
 // Backward finalisation: dweight = sum(g * xhat), dbias = sum(g), the
 // convolution bias gradient sum(dx) (dx = sc * (g - mg - xhat * mgx) summed in
 // fp64), coefficients.
+// With a WgradReduceJob (bb_bn_backward_red): blocks from (C + 3) / 4 on add a preceding board convolution's
+// weight-gradient partials instead -- two independent small passes in one launch.
 __global__ void __launch_bounds__(kBnThreads) bn_finalize_bwd(const double* __restrict__ part, int nb, int C, double M,
                                                               const float* __restrict__ pre_bias,
                                                               const float* __restrict__ w, const float* __restrict__ b,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, float* __restrict__ dw,
                                                               float* __restrict__ db, float* __restrict__ dpb,
-                                                              float* __restrict__ coef) {
+                                                              float* __restrict__ coef, WgradReduceJob job) {
+  const int fin_blocks = (C + 3) / 4;
+  if ((int)blockIdx.x >= fin_blocks) {
+    wgrad_reduce_at(job, ((int)blockIdx.x - fin_blocks) * kBnThreads + threadIdx.x);
+    return;
+  }
   int c;
   double a[kQ];
   if (!channel_sums(part, nb, C, c, a)) return;
@@ -522,12 +548,19 @@ hipError_t bn_forward_t(const void* x, const void* res, int nhwc, int N, int C, 
 template <typename T>
 hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, int HW, const float* pb,
                          const float* w, const float* b, const float* mean, const float* invstd, int relu, double* ws,
-                         void* dx, float* dw, float* db, float* dpb, hipStream_t s, const void* mask, void* gout) {
+                         void* dx, float* dw, float* db, float* dpb, hipStream_t s, const void* mask, void* gout,
+                         const WgradReduceJob* job) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
   launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s, mask);
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, k.part, p.nb, C, (double)N * HW, pb,
-                     w, b, mean, invstd, dw, db, dpb, k.coef);
+  WgradReduceJob jb{};
+  int red_blocks = 0;
+  if (job) {
+    jb = *job;
+    red_blocks = (9 * jb.cout * jb.cin + kBnThreads - 1) / kBnThreads;
+  }
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 3) / 4 + red_blocks), dim3(kBnThreads), 0, s, k.part, p.nb, C,
+                     (double)N * HW, pb, w, b, mean, invstd, dw, db, dpb, k.coef, jb);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc && mask)
     hipLaunchKernelGGL((bn_apply_bwd<T, true, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
@@ -565,11 +598,12 @@ hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
                               int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s,
-                              const void* mask, void* gout) {
+                              const void* mask, void* gout, const WgradReduceJob* job) {
   if (dtype == 1)
     return bn_backward_t<__hip_bfloat16>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s,
-                                         mask, gout);
-  return bn_backward_t<float>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s, mask, gout);
+                                         mask, gout, job);
+  return bn_backward_t<float>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s, mask, gout,
+                              job);
 }
 
 }  // namespace bb

@@ -162,6 +162,22 @@ def _bn_workspace(x: torch.Tensor, nhwc: int) -> torch.Tensor:
     return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=x.device)
 
 
+def _bn_backward_call(x, dy, nhwc, pre_bias, weight, bias, mean, invstd, relu: int, ws, dx, dw, db, dpb, dev):
+    """bb_bn_backward, or bb_bn_backward_red carrying a board convolution's pending weight-gradient reduction
+    (wgrad_piggyback) in its finalisation launch."""
+    n, c, h, w = x.shape
+    lib = L.load()
+    job = _take_pending_reduce(dev)
+    args = (_p(x), _p(dy), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight), _p(bias), _p(mean),
+            _p(invstd), int(relu), _p(ws), _p(dx), _p(dw), _p(db), _p(dpb))
+    if job is None:
+        L.check(lib.bb_bn_backward(*args, _s(dev)), "bb_bn_backward")
+    else:
+        cws, chunks, cin, cout, wl, cdw = job
+        L.check(lib.bb_bn_backward_red(*args, _p(cws), chunks, cin, cout, wl, C.c_void_p(cdw), _s(dev)),
+                "bb_bn_backward_red")
+
+
 class BatchNormReLUFunction(torch.autograd.Function):
     """y = [relu](batch_norm(x + pre_bias, batch statistics)) with running-stat
     update; backward from x and the saved mean / inverse std
@@ -202,10 +218,8 @@ class BatchNormReLUFunction(torch.autograd.Function):
         db = torch.empty_like(bias)
         dpb = torch.empty_like(pre_bias) if pre_bias is not None else None
         ws = _bn_workspace(x, ctx.nhwc)
-        L.check(L.load().bb_bn_backward(_p(x), _p(dy), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w, _p(pre_bias),
-                                        _p(weight), _p(bias), _p(mean), _p(invstd), int(ctx.relu), _p(ws), _p(dx),
-                                        _p(dw), _p(db), _p(dpb), _s(dev)),
-                "bb_bn_backward")
+        _bn_backward_call(x, dy, ctx.nhwc, pre_bias, weight, bias, mean, invstd, int(ctx.relu), ws, dx, dw, db, dpb,
+                          dev)
         return dx, dpb, dw, db, None, None, None, None, None, None
 
 
@@ -266,10 +280,7 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
                     "bb_bn_backward_res")
         else:
             g = torch.ops.aten.threshold_backward(dy, y, 0).contiguous(memory_format=fmt)
-            L.check(L.load().bb_bn_backward(_p(x), _p(g), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w, _p(pre_bias),
-                                            _p(weight), _p(bias), _p(mean), _p(invstd), 0, _p(ws), _p(dx), _p(dw),
-                                            _p(db), _p(dpb), _s(dev)),
-                    "bb_bn_backward")
+            _bn_backward_call(x, g, ctx.nhwc, pre_bias, weight, bias, mean, invstd, 0, ws, dx, dw, db, dpb, dev)
         gres = g
         if ctx.mailbox is not None and ctx.needs_input_grad[2]:
             ctx.mailbox.put(g)  # the block's first convolution adds it to its data gradient
@@ -345,6 +356,63 @@ def _wgrad_deferred(weight: torch.Tensor, dev: torch.device, saved, compute) -> 
         t.record_stream(side)
     st[1] = True
     return True
+
+
+# ---------------------------------------------------------------------------
+# Weight-gradient reductions carried by the next BatchNorm backward: inside ``wgrad_piggyback(device)`` a board
+# convolution's backward launches only the weight-gradient partial-sum kernel and leaves its fixed-order reduction
+# pending; the next BatchNorm backward on the device (the one that always follows a convolution in the CNN's
+# backward) runs it as extra workgroups of its finalisation launch (bb_bn_backward_red): two small launches become
+# one.  Whatever is still pending when the block closes (or when a second convolution comes first) is reduced in
+# a launch of its own, so every weight gradient is complete at the block's exit -- before clip + Adam or a
+# data-parallel all-reduce reads it.  Only for backward passes with no gradient hooks in between (a hook would see
+# the weight gradient before its reduction): PPOAgent opens the block on one rank, or around a data-parallel
+# backward whose all-reduce runs after it.
+# ---------------------------------------------------------------------------
+# A pending job holds the weight gradient by address only: a Python reference would make autograd's
+# AccumulateGrad copy the (not yet reduced) tensor into .grad instead of keeping it; the block's exit checks that
+# every such .grad is the tensor the reduction wrote.
+WGRAD_PIGGYBACK = os.environ.get("BB_WGRAD_PIGGYBACK", "1") != "0"
+_pending_red = {}  # device -> [depth, pending job or None, [(weight, dw address)]]
+
+
+def _flush_reduce(dev, job) -> None:
+    cws, chunks, cin, cout, wl, cdw = job
+    L.check(L.load().bb_conv3x3_wgrad_reduce(_p(cws), chunks, cin, cout, wl, C.c_void_p(cdw), _s(dev)),
+            "bb_conv3x3_wgrad_reduce")
+
+
+def _take_pending_reduce(dev):
+    st = _pending_red.get(torch.device(dev))
+    if not st or st[1] is None:
+        return None
+    job, st[1] = st[1], None
+    return job
+
+
+class wgrad_piggyback:
+    def __init__(self, device: torch.device, enabled: bool = True):
+        self.dev = torch.device(device)
+        self.on = bool(enabled and WGRAD_PIGGYBACK and self.dev.type == "cuda")
+
+    def __enter__(self):
+        if self.on:
+            _pending_red.setdefault(self.dev, [0, None, []])[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            st = _pending_red[self.dev]
+            st[0] -= 1
+            job = _take_pending_reduce(self.dev)
+            if job is not None:
+                _flush_reduce(self.dev, job)
+            checks, st[2] = st[2], []
+            for weight, addr in checks:
+                if exc[0] is None and (weight.grad is None or weight.grad.data_ptr() != addr):
+                    raise L.BBNativeError("wgrad_piggyback: autograd copied a pending weight gradient; open the "
+                                          "block only around a backward whose parameters' .grad are all None")
+        return False
 
 
 def conv3x3_fusable(x: torch.Tensor, conv) -> bool:
@@ -468,7 +536,19 @@ class Conv3x3Function(torch.autograd.Function):
                         "bb_conv3x3_wgrad")
                 return g
 
-            if not _wgrad_deferred(weight, dev, (x, dy), wgrad):
+            st = _pending_red.get(torch.device(dev))
+            if st and st[0] > 0 and not _wg_active.get(dev, [0])[0] > 0:
+                # partial sums now, their reduction in the next BatchNorm backward's finalisation launch
+                prev = _take_pending_reduce(dev)
+                if prev is not None:
+                    _flush_reduce(dev, prev)
+                ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+                dw = torch.empty_like(weight, dtype=torch.float32)
+                L.check(lib.bb_conv3x3_wgrad_partial(_p(x), _p(dy), n, cin, cout, _p(ws), _s(dev)),
+                        "bb_conv3x3_wgrad_partial")
+                st[1] = (ws, lib.bb_conv3x3_wgrad_chunks(n, cin, cout), cin, cout, _w_layout(dw), dw.data_ptr())
+                st[2].append((weight, dw.data_ptr()))
+            elif not _wgrad_deferred(weight, dev, (x, dy), wgrad):
                 dw = wgrad()
         return dx, dw, None, None
 

@@ -148,6 +148,8 @@ SIGNATURES = {
                                     _F, _P, _P, _P]),
     "bb_bn_backward": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                  _P]),
+    "bb_bn_backward_red": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
+                                     _P, _I32, _I32, _I32, _I32, _P, _P]),
     "bb_bn_backward_res": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P]),
     "bb_conv3x3_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
@@ -156,6 +158,9 @@ SIGNATURES = {
     "bb_conv3x3_forward": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_conv3x3_forward_add": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
     "bb_conv3x3_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _P, _P]),
+    "bb_conv3x3_wgrad_chunks": (C.c_int32, [_I32, _I32, _I32]),
+    "bb_conv3x3_wgrad_partial": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
+    "bb_conv3x3_wgrad_reduce": (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P]),
     "bb_conv3x3_f32_prep": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "bb_conv3x3_f32_forward": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "bb_linear_f32": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P]),

@@ -40,7 +40,8 @@ extern "C" {
                               7: bb_ppo_loss_forward_bf16 / _backward_bf16;
                               8: bb_dropout_forward, bb_linear_bgrad, bb_linear_wgrad, bb_linear_n1_*;
                                  bb_conv_in_forward / _wgrad; bb_bn_backward_res; bb_ppo_loss_fused and the
-                                 loss forward's d_cnt (one launch, the statistics finalised in it) */
+                                 loss forward's d_cnt (one launch, the statistics finalised in it);
+                                 bb_conv3x3_wgrad_partial / _reduce / _chunks, bb_bn_backward_red */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -330,6 +331,13 @@ int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhw
                    const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
                    int32_t relu, double* d_ws, void* d_dx, float* d_dweight, float* d_dbias,
                    float* d_dpre_bias, void* stream);
+/* bb_bn_backward with a board convolution's weight-gradient reduction (bb_conv3x3_wgrad_reduce's arguments)
+ * run as extra workgroups of the BatchNorm finalisation's launch: two small launches in one (ABI 8). */
+int bb_bn_backward_red(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW,
+                       const float* d_pre_bias, const float* d_weight, const float* d_bias, const float* d_save_mean,
+                       const float* d_save_invstd, int32_t relu, double* d_ws, void* d_dx, float* d_dweight,
+                       float* d_dbias, float* d_dpre_bias, const float* d_conv_ws, int32_t conv_chunks,
+                       int32_t conv_cin, int32_t conv_cout, int32_t conv_w_layout, float* d_conv_dw, void* stream);
 /* The backward of bb_bn_forward_res with its ReLU: bb_bn_backward (relu = 0) over g = (y > 0 ? dy : 0), y the
  * forward's output (torch's threshold_backward), the mask applied inside the reduction and elementwise
  * passes instead of a pass of its own; g, the residual's gradient, is written to d_gres when non-NULL
@@ -416,6 +424,14 @@ int bb_conv3x3_forward_add(const void* d_x, const void* d_w, int32_t N, int32_t 
                            const void* d_add, void* d_y, void* stream);
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
+/* bb_conv3x3_wgrad in two parts (ABI 8): the partial-sum kernel into d_ws, then the fixed-order sum of its
+ * bb_conv3x3_wgrad_chunks(N, cin, cout) chunks into d_dw (alone, or inside bb_bn_backward_red); together
+ * bit-identical to bb_conv3x3_wgrad. */
+int32_t bb_conv3x3_wgrad_chunks(int32_t N, int32_t cin, int32_t cout);
+int bb_conv3x3_wgrad_partial(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
+                             void* stream);
+int bb_conv3x3_wgrad_reduce(const float* d_ws, int32_t chunks, int32_t cin, int32_t cout, int32_t w_layout,
+                            float* d_dw, void* stream);
 
 /* The same 3x3 convolutions in fp32 (no autocast: the reference's own precision), for (cin, cout) =
  * (128, 128), (64, 128) and (128, 64) (the last is the data gradient of the 64 -> 128 layer).  Every output

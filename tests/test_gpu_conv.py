@@ -301,3 +301,47 @@ def test_network_conv_in_equals_miopen(cuda, monkeypatch):
         if name.endswith(".bias") and res[True][2][name[:-5] + ".weight"].dim() == 4:
             continue  # a conv bias before BatchNorm: zero up to noise
         assert float((gr - ref).norm() / ref.norm().clamp_min(1e-30)) < 0.5, name
+
+
+def test_wgrad_piggyback_equals_plain(cuda, monkeypatch):
+    """The board convolutions' weight-gradient reductions carried by the next BatchNorm backward's finalisation
+    launch (wgrad_piggyback, bb_bn_backward_red) == the plain two-launch weight gradient, bit for bit: the whole
+    bf16 CNN's parameter gradients and the BatchNorm outputs; a pending reduction with no BatchNorm after it is
+    flushed when the block closes."""
+    import models.network as N
+    from runtime import kernels as K
+
+    torch.manual_seed(5)
+    net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    net.train()
+    x = (torch.rand((256, 4, 8, 8), device=cuda) < 0.4).float()
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+    res = {}
+    for on in (True, False):
+        net.load_state_dict(state0)
+        for p in net.parameters():
+            p.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            lo, va = net.raw(x)
+        with K.wgrad_piggyback(cuda, enabled=on):
+            (lo.float().square().mean() + va.float().sum()).backward()
+        res[on] = {n: p.grad.clone() for n, p in net.named_parameters()}
+    for n, g in res[True].items():
+        if n.startswith("conv_encoder.0."):  # the input layer's own reduction is not carried; MIOpen-free either way
+            assert torch.equal(g, res[False][n]), n
+            continue
+        assert torch.equal(g, res[False][n]), n
+    # a lone convolution: its pending reduction is flushed at the block's exit
+    conv = [m for m in net.conv_encoder.modules() if isinstance(m, torch.nn.Conv2d) and m.in_channels == 128][0]
+    xb = torch.randn((64, 128, 8, 8), device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    dy = torch.randn((64, 128, 8, 8), device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for on in (True, False):
+        w = conv.weight.detach().clone().requires_grad_(True)
+        with K.wgrad_piggyback(cuda, enabled=on):
+            K.Conv3x3Function.apply(xb, w).backward(dy)
+        outs.append(w.grad)
+    assert torch.equal(outs[0], outs[1])
