@@ -732,7 +732,7 @@ extern "C" int bb_bn_backward_res(const void* d_x, const void* d_dy, const void*
                                   void* d_gres, void* stream) {
   int rc = bn_check(dtype, nhwc, N, C, HW);
   if (rc != BB_OK) return rc;
-  if (!d_x || !d_dy || !d_y || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx)
+  if (!d_x || !d_dy || !d_y || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx || !d_gres)
     return fail(nullptr, BB_ERR_ARG, "bb_bn_backward_res: NULL argument");
   if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
   hipError_t st = launch_bn_backward(d_x, d_dy, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, d_save_mean,

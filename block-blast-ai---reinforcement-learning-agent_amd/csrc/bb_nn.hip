@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
                                                              const float* __restrict__ w, const float* __restrict__ b,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd, int relu,
-                                                             const void* __restrict__ mask,
+                                                             const void* __restrict__ mask, void* __restrict__ gout,
                                                              double* __restrict__ part) {
   __shared__ double red[kQ][kBnThreads / 64];
   constexpr int V = Vec<T>::N;
@@ -177,7 +177,10 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nchw(const void* __restr
       float fx[V], fg[V];
       Vec<T>::load(x, i, fx);
       if (BWD) Vec<T>::load(dy, i, fg);
-      if (BWD && MASK) mask_grad<T>(mask, i, fg);
+      if (BWD && MASK) {
+        mask_grad<T>(mask, i, fg);
+        Vec<T>::store(gout, i, fg);  // the masked gradient, for the apply pass and the residual (exact in T)
+      }
 #pragma unroll
       for (int j = 0; j < V; ++j) accumulate<T, BWD>(fx[j], BWD ? fg[j] : 0.f, k, relu, s, q, t);
     }
@@ -203,7 +206,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
                                                              const float* __restrict__ w, const float* __restrict__ b,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd, int relu,
-                                                             const void* __restrict__ mask,
+                                                             const void* __restrict__ mask, void* __restrict__ gout,
                                                              double* __restrict__ part) {
   constexpr int V = Vec<T>::N;
   constexpr int NQ = BWD ? kQ : 2;  // the forward has no third quantity
@@ -227,7 +230,10 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_nhwc(const void* __restr
       if (n < R) {
         Vec<T>::load(x, (int64_t)n * cpr + kc, fx[u]);
         if (BWD) Vec<T>::load(dy, (int64_t)n * cpr + kc, fg[u]);
-        if (BWD && MASK) mask_grad<T>(mask, (int64_t)n * cpr + kc, fg[u]);
+        if (BWD && MASK) {
+          mask_grad<T>(mask, (int64_t)n * cpr + kc, fg[u]);
+          Vec<T>::store(gout, (int64_t)n * cpr + kc, fg[u]);  // the masked gradient (exact in T)
+        }
       }
     }
 #pragma unroll
@@ -403,11 +409,10 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restric
   }
 }
 
-template <typename T, bool NHWC, bool MASK = false>
+template <typename T, bool NHWC>
 __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restrict__ x, const void* __restrict__ dy,
                                                            void* __restrict__ dx, int64_t total, int C, int cpr,
-                                                           int relu, const float* __restrict__ coef,
-                                                           const void* __restrict__ mask, void* __restrict__ gout) {
+                                                           int relu, const float* __restrict__ coef) {
   constexpr int V = Vec<T>::N;
   constexpr int NC = NHWC ? V : 1;
   const float4* cf = reinterpret_cast<const float4*>(coef);
@@ -430,10 +435,6 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restric
     float fx[V], fg[V];
     Vec<T>::load(x, i, fx);
     Vec<T>::load(dy, i, fg);
-    if (MASK) {
-      mask_grad<T>(mask, i, fg);
-      if (gout) Vec<T>::store(gout, i, fg);  // the residual's gradient (values of dy or 0: exact in T)
-    }
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float4& a = k0[NHWC ? j : 0];  // {pb, mu, sc, sh}
@@ -495,21 +496,21 @@ int grid_for_elems(int64_t chunks, int nhwc) {
 template <typename T, bool BWD>
 void launch_reduce(const Plan& p, int nhwc, const void* x, const void* dy, int N, int C, int HW, const float* pb,
                    const float* w, const float* b, const float* mean, const float* invstd, int relu, double* part,
-                   hipStream_t s, const void* mask = nullptr) {
+                   hipStream_t s, const void* mask = nullptr, void* gout = nullptr) {
   if (nhwc) {
     if (BWD && mask)
       hipLaunchKernelGGL((bn_reduce_nhwc<T, BWD, true>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N * HW, C, pb, w, b,
-                         mean, invstd, relu, mask, part);
+                         mean, invstd, relu, mask, gout, part);
     else
       hipLaunchKernelGGL((bn_reduce_nhwc<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N * HW, C, pb, w, b, mean,
-                         invstd, relu, nullptr, part);
+                         invstd, relu, nullptr, nullptr, part);
   } else {
     if (BWD && mask)
       hipLaunchKernelGGL((bn_reduce_nchw<T, BWD, true>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N, C, HW, pb, w, b,
-                         mean, invstd, relu, mask, part);
+                         mean, invstd, relu, mask, gout, part);
     else
       hipLaunchKernelGGL((bn_reduce_nchw<T, BWD>), p.rgrid, dim3(kBnThreads), 0, s, x, dy, N, C, HW, pb, w, b, mean,
-                         invstd, relu, nullptr, part);
+                         invstd, relu, nullptr, nullptr, part);
   }
 }
 
@@ -552,7 +553,10 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
                          const WgradReduceJob* job) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
-  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s, mask);
+  // with a mask (the ResidualBlock tail): the reduction writes the masked gradient g to gout, and the
+  // elementwise pass reads g as its dy (no mask there)
+  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s, mask, gout);
+  if (mask) dy = gout;
   WgradReduceJob jb{};
   int red_blocks = 0;
   if (job) {
@@ -562,18 +566,12 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
   hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 3) / 4 + red_blocks), dim3(kBnThreads), 0, s, k.part, p.nb, C,
                      (double)N * HW, pb, w, b, mean, invstd, dw, db, dpb, k.coef, jb);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
-  if (nhwc && mask)
-    hipLaunchKernelGGL((bn_apply_bwd<T, true, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
-                       k.coef, mask, gout);
-  else if (nhwc)
+  if (nhwc)
     hipLaunchKernelGGL((bn_apply_bwd<T, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
-                       k.coef, nullptr, nullptr);
-  else if (mask)
-    hipLaunchKernelGGL((bn_apply_bwd<T, false, true>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
-                       k.coef, mask, gout);
+                       k.coef);
   else
     hipLaunchKernelGGL((bn_apply_bwd<T, false>), ge, dim3(kBnThreads), 0, s, x, dy, dx, p.chunks, C, p.cpr, relu,
-                       k.coef, nullptr, nullptr);
+                       k.coef);
   return hipGetLastError();
 }
 

@@ -223,9 +223,11 @@ class BatchNormReLUFunction(torch.autograd.Function):
         return dx, dpb, dw, db, None, None, None, None, None, None
 
 
-# ResidualBlock tail backward on bb_bn_backward_res (opt-in: 1.619 against 1.613 ms per step, three interleaved
-# repeats, profiles/r05/rm/ -- the masked passes grow by about what the threshold_backward pass took)
-RES_MASK = os.environ.get("BB_RES_MASK", "0") == "1"
+# ResidualBlock tail backward on bb_bn_backward_res: the ReLU mask applied in the BatchNorm reduction, which
+# writes the masked gradient for the elementwise pass (0: threshold_backward + bb_bn_backward, for A/B).
+# 1.575-1.579 against 1.579-1.583 ms per step, three interleaved repeats, 2 launches fewer
+# (profiles/r05/rm/r05rm2_ab.log; the first form, mask applied in both passes, was 1.619 against 1.613)
+RES_MASK = os.environ.get("BB_RES_MASK", "1") != "0"
 
 
 class BatchNormAddReLUFunction(torch.autograd.Function):
@@ -273,7 +275,7 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
         dpb = torch.empty_like(pre_bias) if pre_bias is not None else None
         ws = _bn_workspace(x, ctx.nhwc)
         if RES_MASK:  # the ReLU's mask from the saved output inside the BatchNorm passes (threshold_backward)
-            g = torch.empty_like(x) if ctx.needs_input_grad[2] else None  # the residual's gradient
+            g = torch.empty_like(x)  # the masked gradient: the residual's, and the elementwise pass's input
             L.check(L.load().bb_bn_backward_res(_p(x), _p(dy), _p(y), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w,
                                                 _p(pre_bias), _p(weight), _p(bias), _p(mean), _p(invstd), _p(ws),
                                                 _p(dx), _p(dw), _p(db), _p(dpb), _p(g), _s(dev)),

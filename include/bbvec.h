@@ -339,9 +339,9 @@ int bb_bn_backward_red(const void* d_x, const void* d_dy, int32_t dtype, int32_t
                        float* d_dbias, float* d_dpre_bias, const float* d_conv_ws, int32_t conv_chunks,
                        int32_t conv_cin, int32_t conv_cout, int32_t conv_w_layout, float* d_conv_dw, void* stream);
 /* The backward of bb_bn_forward_res with its ReLU: bb_bn_backward (relu = 0) over g = (y > 0 ? dy : 0), y the
- * forward's output (torch's threshold_backward), the mask applied inside the reduction and elementwise
- * passes instead of a pass of its own; g, the residual's gradient, is written to d_gres when non-NULL
- * (x's shape, dtype and layout).  Three launches, as bb_bn_backward. */
+ * forward's output (torch's threshold_backward): the reduction pass applies the mask and writes g to d_gres (x's
+ * shape, dtype and layout; required), the elementwise pass reads it -- three launches, as bb_bn_backward, and no
+ * pass of the mask's own.  g is also the residual's gradient. */
 int bb_bn_backward_res(const void* d_x, const void* d_dy, const void* d_y, int32_t dtype, int32_t nhwc, int32_t N,
                        int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias,
                        const float* d_save_mean, const float* d_save_invstd, double* d_ws, void* d_dx,
