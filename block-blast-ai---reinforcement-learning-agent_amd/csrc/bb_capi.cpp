@@ -729,15 +729,21 @@ extern "C" int bb_bn_backward_res(const void* d_x, const void* d_dy, const void*
                                   int32_t N, int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                                   const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
                                   double* d_ws, void* d_dx, float* d_dweight, float* d_dbias, float* d_dpre_bias,
-                                  void* d_gres, void* stream) {
+                                  void* d_gres, const float* d_conv_ws, int32_t conv_chunks, int32_t conv_cin,
+                                  int32_t conv_cout, int32_t conv_w_layout, float* d_conv_dw, void* stream) {
   int rc = bn_check(dtype, nhwc, N, C, HW);
   if (rc != BB_OK) return rc;
   if (!d_x || !d_dy || !d_y || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx || !d_gres)
     return fail(nullptr, BB_ERR_ARG, "bb_bn_backward_res: NULL argument");
   if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
+  const bool red = d_conv_ws != nullptr;
+  if (red && (!d_conv_dw || conv_chunks <= 0 || (conv_w_layout != 0 && conv_w_layout != 1) ||
+              !conv3x3_supported(conv_cin, conv_cout)))
+    return fail(nullptr, BB_ERR_ARG, "bb_bn_backward_res: bad convolution reduction arguments");
+  const WgradReduceJob job{d_conv_ws, conv_chunks, conv_cout, conv_cin, conv_w_layout, d_conv_dw};
   hipError_t st = launch_bn_backward(d_x, d_dy, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, d_save_mean,
                                      d_save_invstd, 0, d_ws, d_dx, d_dweight, d_dbias, d_dpre_bias, (hipStream_t)stream,
-                                     d_y, d_gres);
+                                     d_y, d_gres, red ? &job : nullptr);
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_backward_res");
   return BB_OK;
 }
@@ -1047,6 +1053,21 @@ extern "C" int bb_conv_in_forward(const float* d_x, int32_t x_nhwc, const float*
   if (st == hipErrorInvalidValue)
     return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward: wl must be 0 or 1, x and y 16-byte aligned");
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_forward");
+  return BB_OK;
+}
+
+extern "C" int bb_conv_in_forward_prep(const float* d_x, int32_t x_nhwc, const float* d_w, int32_t wl, int32_t N,
+                                       void* d_y, int32_t count, const float* const* h_w, const int32_t* h_cin,
+                                       const int32_t* h_cout, const int32_t* h_w_layout, void* const* h_wf,
+                                       void* const* h_wd, void* stream) {
+  if (!d_x || !d_w || !d_y || !h_w || !h_cin || !h_cout || !h_w_layout || !h_wf || !h_wd)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward_prep: NULL argument");
+  if (N <= 0) return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward_prep: N must be positive");
+  hipError_t st = launch_conv_in_forward_prep(d_x, x_nhwc, d_w, wl, N, d_y, count, h_w, h_cin, h_cout, h_w_layout, h_wf,
+                                              h_wd, (hipStream_t)stream);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv_in_forward_prep: bad layout, alignment or prep table (1 to 16 layers)");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv_in_forward_prep");
   return BB_OK;
 }
 

@@ -86,11 +86,11 @@ struct PrepTable {
   int count;
 };
 
-__global__ void __launch_bounds__(kThreads) conv_prep_multi_kernel(const PrepTable tab) {
+__device__ __forceinline__ void prep_block(const PrepTable& tab, int blk) {  // workgroup blk of the table's launch
   int l = 0;
-  while (l + 1 < tab.count && tab.block0[l + 1] <= (int)blockIdx.x) ++l;
+  while (l + 1 < tab.count && tab.block0[l + 1] <= blk) ++l;
   const int cout = tab.cout[l], cin = tab.cin[l], wl = tab.wl[l];
-  const int i = (blockIdx.x - tab.block0[l]) * kThreads + threadIdx.x;
+  const int i = (blk - tab.block0[l]) * kThreads + threadIdx.x;
   if (i >= cout * cin * 9) return;
   const int co = i / (9 * cin);
   const int t = wl ? (i / cin) % 9 : i % 9;
@@ -99,6 +99,12 @@ __global__ void __launch_bounds__(kThreads) conv_prep_multi_kernel(const PrepTab
   tab.wf[l][(t * cout + co) * cin + ci] = b;
   tab.wd[l][((8 - t) * cin + ci) * cout + co] = b;
 }
+
+__global__ void __launch_bounds__(kThreads) conv_prep_multi_kernel(const PrepTable tab) { prep_block(tab, blockIdx.x); }
+
+// A prep table's launch geometry (PrepTable.block0); -1: a layer the HIP convolutions do not take
+int build_prep_table(PrepTable& tab, int count, const float* const* w, const int32_t* cin, const int32_t* cout,
+                     const int32_t* wl, void* const* wf, void* const* wd);
 
 // LDS image of pixel rows of C bf16 channels: 16-byte chunk c of row r sits at
 // chunk c ^ key(r).  The B fragment of mfma_f32_16x16x32_bf16 puts pixel n of a
@@ -865,13 +871,21 @@ __device__ __forceinline__ void in_weight_frags(const float* __restrict__ w, int
     }
 }
 
+// With prep_blocks > 0 the launch's last prep_blocks workgroups build the other layers' bf16 weight images
+// (conv_prep_multi's work, independent of this layer: both run at the start of the forward, in one launch).
 __global__ void __launch_bounds__(256) conv_in_fwd_kernel(const float* __restrict__ x, int x_nhwc,
                                                           const float* __restrict__ w, int wl, int nb,
-                                                          uint16_t* __restrict__ y) {
+                                                          uint16_t* __restrict__ y, const PrepTable pt,
+                                                          int prep_blocks) {
   __shared__ float4 xpad[kInWaves][100];      // per wave: [(r + 1) * 10 + c + 1] -> 4 channels
   __shared__ uint4 ost[kInWaves][64 * 8];     // per wave: [pixel][16-B chunk ^ (pixel & 7)] of 8 channels
+  const int fwd_blocks = (int)gridDim.x - prep_blocks;
+  if ((int)blockIdx.x >= fwd_blocks) {
+    prep_block(pt, (int)blockIdx.x - fwd_blocks);
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
-  const int stride = gridDim.x * kInWaves;
+  const int stride = fwd_blocks * kInWaves;
   int b = blockIdx.x * kInWaves + wave;
   // the first board's load in flight with the weight fragments' (every wave works alone: no barrier)
   float4 xv = b < nb ? reinterpret_cast<const float4*>(x + (size_t)b * 256)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1065,15 +1079,14 @@ hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* 
   return hipGetLastError();
 }
 
-hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
-                                     const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s) {
-  if (count <= 0 || count > kPrepMax) return hipErrorInvalidValue;
-  PrepTable tab;
+namespace {
+int build_prep_table(PrepTable& tab, int count, const float* const* w, const int32_t* cin, const int32_t* cout,
+                     const int32_t* wl, void* const* wf, void* const* wd) {
+  if (count <= 0 || count > kPrepMax) return -1;
   tab.count = count;
   int blocks = 0;
   for (int l = 0; l < count; ++l) {
-    if (!w[l] || !wf[l] || !wd[l] || !conv3x3_supported(cin[l], cout[l]) || (wl[l] != 0 && wl[l] != 1))
-      return hipErrorInvalidValue;
+    if (!w[l] || !wf[l] || !wd[l] || !conv3x3_supported(cin[l], cout[l]) || (wl[l] != 0 && wl[l] != 1)) return -1;
     tab.w[l] = w[l];
     tab.wf[l] = static_cast<uint16_t*>(wf[l]);
     tab.wd[l] = static_cast<uint16_t*>(wd[l]);
@@ -1084,6 +1097,15 @@ hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int
     blocks += (cout[l] * cin[l] * 9 + kThreads - 1) / kThreads;
   }
   tab.block0[count] = blocks;
+  return blocks;
+}
+}  // namespace
+
+hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
+                                     const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s) {
+  PrepTable tab;
+  const int blocks = build_prep_table(tab, count, w, cin, cout, wl, wf, wd);
+  if (blocks <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(conv_prep_multi_kernel, dim3(blocks), dim3(kThreads), 0, s, tab);
   return hipGetLastError();
 }
@@ -1127,7 +1149,24 @@ hipError_t launch_conv_in_forward(const float* x, int x_nhwc, const float* w, in
       (reinterpret_cast<uintptr_t>(y) & 15))
     return hipErrorInvalidValue;
   const int blocks = std::min((nb + kInWaves - 1) / kInWaves, kInFwdBlocks);
-  hipLaunchKernelGGL(conv_in_fwd_kernel, dim3(blocks), dim3(256), 0, s, x, x_nhwc ? 1 : 0, w, wl, nb, (uint16_t*)y);
+  PrepTable pt{};
+  hipLaunchKernelGGL(conv_in_fwd_kernel, dim3(blocks), dim3(256), 0, s, x, x_nhwc ? 1 : 0, w, wl, nb, (uint16_t*)y, pt,
+                     0);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_in_forward_prep(const float* x, int x_nhwc, const float* w, int wl, int nb, void* y, int count,
+                                       const float* const* pw, const int32_t* cin, const int32_t* cout,
+                                       const int32_t* pwl, void* const* wf, void* const* wd, hipStream_t s) {
+  if (nb <= 0 || !x || !w || !y || (wl != 0 && wl != 1) || (reinterpret_cast<uintptr_t>(x) & 15) ||
+      (reinterpret_cast<uintptr_t>(y) & 15) || count <= 0 || count > kPrepMax)
+    return hipErrorInvalidValue;
+  PrepTable pt;
+  const int pblocks = build_prep_table(pt, count, pw, cin, cout, pwl, wf, wd);
+  if (pblocks <= 0) return hipErrorInvalidValue;
+  const int blocks = std::min((nb + kInWaves - 1) / kInWaves, kInFwdBlocks);
+  hipLaunchKernelGGL(conv_in_fwd_kernel, dim3(blocks + pblocks), dim3(256), 0, s, x, x_nhwc ? 1 : 0, w, wl, nb,
+                     (uint16_t*)y, pt, pblocks);
   return hipGetLastError();
 }
 

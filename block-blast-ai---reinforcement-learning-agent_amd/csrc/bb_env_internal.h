@@ -138,6 +138,9 @@ hipError_t launch_conv3x3_wgrad_reduce(const float* ws, int used, int cin, int c
 // the input layer, conv 4 -> 64 (x f32 NCHW or NHWC, w f32 [64][4][3][3] wl 0 or [64][3][3][4] wl 1)
 int64_t conv_in_wgrad_workspace_bytes(int nb);
 hipError_t launch_conv_in_forward(const float* x, int x_nhwc, const float* w, int wl, int nb, void* y, hipStream_t s);
+hipError_t launch_conv_in_forward_prep(const float* x, int x_nhwc, const float* w, int wl, int nb, void* y, int count,
+                                       const float* const* pw, const int32_t* cin, const int32_t* cout,
+                                       const int32_t* pwl, void* const* wf, void* const* wd, hipStream_t s);
 hipError_t launch_conv_in_wgrad(const float* x, int x_nhwc, const void* dy, int nb, float* ws, int wl, float* dw,
                                 hipStream_t s);
 

@@ -115,10 +115,13 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> 
     if _hip_conv_on(x):
         from runtime.kernels import ConvInFunction, Conv3x3Function, conv3x3_fusable, conv_in_fusable
 
+        prep = images.get("prep") if images else None  # the weight images' launch, if not made yet
         if conv3x3_fusable(x, conv):
+            if prep is not None:
+                prep.run()
             return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox)
-        if conv_in_fusable(x, conv):  # the 4 -> 64 input layer: f32 boards in, bf16 NHWC out
-            return ConvInFunction.apply(x, conv.weight)
+        if conv_in_fusable(x, conv):  # the 4 -> 64 input layer: f32 boards in, bf16 NHWC out (+ the images)
+            return ConvInFunction.apply(x, conv.weight, prep)
     elif _f32_conv_on(x, conv):
         from runtime.kernels import Conv3x3F32Function
 
@@ -362,6 +365,16 @@ class BlockBlastNetwork(nn.Module):
         convs = [m for m in self.conv_encoder.modules() if isinstance(m, nn.Conv2d) and conv3x3_fusable(probe, m)]
         if not convs or len(convs) > 16:
             return None
+        from runtime.kernels import conv_in_fusable
+
+        first = self.conv_encoder[0] if len(self.conv_encoder) else None
+        if isinstance(first, nn.Conv2d) and conv_in_fusable(x, first):
+            # the input layer's forward launch builds the images too (bb_conv_in_forward_prep); a HIP
+            # convolution reached first launches them on its own
+            imgs, job = conv3x3_prep_multi([c.weight for c in convs], defer=True)
+            out = dict(zip(convs, imgs))
+            out["prep"] = job
+            return out
         return dict(zip(convs, conv3x3_prep_multi([c.weight for c in convs])))
 
     def _trunk(self, x: torch.Tensor):

@@ -276,9 +276,13 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
         ws = _bn_workspace(x, ctx.nhwc)
         if RES_MASK:  # the ReLU's mask from the saved output inside the BatchNorm passes (threshold_backward)
             g = torch.empty_like(x)  # the masked gradient: the residual's, and the elementwise pass's input
+            job = _take_pending_reduce(dev)  # a convolution's weight-gradient reduction, carried along
+            red = (None, 0, 0, 0, 0, None) if job is None else job
             L.check(L.load().bb_bn_backward_res(_p(x), _p(dy), _p(y), _BN_DTYPES[x.dtype], ctx.nhwc, n, c, h * w,
                                                 _p(pre_bias), _p(weight), _p(bias), _p(mean), _p(invstd), _p(ws),
-                                                _p(dx), _p(dw), _p(db), _p(dpb), _p(g), _s(dev)),
+                                                _p(dx), _p(dw), _p(db), _p(dpb), _p(g), _p(red[0]), red[1], red[2],
+                                                red[3], red[4], None if red[5] is None else C.c_void_p(red[5]),
+                                                _s(dev)),
                     "bb_bn_backward_res")
         else:
             g = torch.ops.aten.threshold_backward(dy, y, 0).contiguous(memory_format=fmt)
@@ -454,13 +458,19 @@ class ConvInFunction(torch.autograd.Function):
     only (the input is data)."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, prep: Optional["PrepJob"] = None):
         _need_cuda(x, weight)
         nhwc = 0 if x.is_contiguous() else 1
         wl = _w_layout(weight)
         n = x.shape[0]
         y = torch.empty((n, 64, 8, 8), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-        L.check(L.load().bb_conv_in_forward(_p(x), nhwc, _p(weight), wl, n, _p(y), _s(x.device)), "bb_conv_in_forward")
+        if prep is not None and not prep.done:  # the other layers' weight images in the same launch
+            L.check(L.load().bb_conv_in_forward_prep(_p(x), nhwc, _p(weight), wl, n, _p(y), *prep.args, _s(x.device)),
+                    "bb_conv_in_forward_prep")
+            prep.done = True
+        else:
+            L.check(L.load().bb_conv_in_forward(_p(x), nhwc, _p(weight), wl, n, _p(y), _s(x.device)),
+                    "bb_conv_in_forward")
         ctx.save_for_backward(x, weight)
         ctx.nhwc, ctx.wl = nhwc, wl
         return y
@@ -469,7 +479,7 @@ class ConvInFunction(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         if not ctx.needs_input_grad[1]:
-            return None, None
+            return None, None, None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n = x.shape[0]
         lib = L.load()
@@ -477,7 +487,7 @@ class ConvInFunction(torch.autograd.Function):
         dw = torch.empty_like(weight)
         L.check(lib.bb_conv_in_wgrad(_p(x), ctx.nhwc, _p(dy), n, _p(ws), ctx.wl, _p(dw), _s(x.device)),
                 "bb_conv_in_wgrad")
-        return None, dw
+        return None, dw, None
 
 
 class Conv3x3Function(torch.autograd.Function):
@@ -641,9 +651,29 @@ class GradMailbox:
         return g
 
 
-def conv3x3_prep_multi(weights):
+class PrepJob:
+    """The table of a bb_conv3x3_prep_multi launch not yet made (conv3x3_prep_multi(..., defer=True)): the input
+    layer's forward launch carries it (bb_conv_in_forward_prep), or run() launches it on its own."""
+
+    def __init__(self, weights, imgs):
+        k = len(weights)
+        i32 = C.c_int32 * k
+        self.dev = weights[0].device
+        self.keep = (weights, imgs)
+        self.args = (k, _ptrs(weights), i32(*[w.shape[1] for w in weights]), i32(*[w.shape[0] for w in weights]),
+                     i32(*[_w_layout(w) for w in weights]), _ptrs([a for a, _ in imgs]), _ptrs([b for _, b in imgs]))
+        self.done = False
+
+    def run(self) -> None:
+        if not self.done:
+            L.check(L.load().bb_conv3x3_prep_multi(*self.args, _s(self.dev)), "bb_conv3x3_prep_multi")
+            self.done = True
+
+
+def conv3x3_prep_multi(weights, defer: bool = False):
     """bb_conv3x3_prep of every weight in one launch (bb_conv3x3_prep_multi):
-    [(forward image, data-gradient image)] per weight, bf16."""
+    [(forward image, data-gradient image)] per weight, bf16.  defer: return (images, PrepJob) with nothing
+    launched yet."""
     k = len(weights)
     if not 0 < k <= 16:
         raise L.BBNativeError("conv3x3_prep_multi: 1 to 16 layers")
@@ -653,11 +683,10 @@ def conv3x3_prep_multi(weights):
     for w in weights:
         n = w.shape[0] * w.shape[1] * 9
         imgs.append((torch.empty(n, dtype=torch.bfloat16, device=dev), torch.empty(n, dtype=torch.bfloat16, device=dev)))
-    i32 = C.c_int32 * k
-    L.check(L.load().bb_conv3x3_prep_multi(k, _ptrs(weights), i32(*[w.shape[1] for w in weights]),
-                                           i32(*[w.shape[0] for w in weights]), i32(*[_w_layout(w) for w in weights]),
-                                           _ptrs([a for a, _ in imgs]), _ptrs([b for _, b in imgs]), _s(dev)),
-            "bb_conv3x3_prep_multi")
+    job = PrepJob(weights, imgs)
+    if defer:
+        return imgs, job
+    job.run()
     return imgs
 
 

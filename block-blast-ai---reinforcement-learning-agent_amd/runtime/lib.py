@@ -151,7 +151,7 @@ SIGNATURES = {
     "bb_bn_backward_red": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
                                      _P, _I32, _I32, _I32, _I32, _P, _P]),
     "bb_bn_backward_res": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                     _P, _P]),
+                                     _P, _P, _I32, _I32, _I32, _I32, _P, _P]),
     "bb_conv3x3_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
     "bb_conv3x3_prep": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "bb_conv3x3_prep_multi": (C.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P]),
@@ -178,6 +178,7 @@ SIGNATURES = {
     "bb_conv_in_wgrad_workspace_bytes": (C.c_int64, [_I32]),
     "bb_conv_in_forward": (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     "bb_conv_in_wgrad": (C.c_int, [_P, _I32, _P, _I32, _P, _I32, _P, _P]),
+    "bb_conv_in_forward_prep": (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "bb_linear_n1_workspace_bytes": (C.c_int64, [_I32, _I32]),
     "bb_linear_n1_counters": (C.c_int32, [_I32]),
     "bb_linear_n1_forward": (C.c_int, [_P, _P, _P, _I32, _I32, _P, _P]),

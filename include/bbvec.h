@@ -41,7 +41,8 @@ extern "C" {
                               8: bb_dropout_forward, bb_linear_bgrad, bb_linear_wgrad, bb_linear_n1_*;
                                  bb_conv_in_forward / _wgrad; bb_bn_backward_res; bb_ppo_loss_fused and the
                                  loss forward's d_cnt (one launch, the statistics finalised in it);
-                                 bb_conv3x3_wgrad_partial / _reduce / _chunks, bb_bn_backward_red */
+                                 bb_conv3x3_wgrad_partial / _reduce / _chunks, bb_bn_backward_red,
+                                 bb_conv_in_forward_prep */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -341,11 +342,14 @@ int bb_bn_backward_red(const void* d_x, const void* d_dy, int32_t dtype, int32_t
 /* The backward of bb_bn_forward_res with its ReLU: bb_bn_backward (relu = 0) over g = (y > 0 ? dy : 0), y the
  * forward's output (torch's threshold_backward): the reduction pass applies the mask and writes g to d_gres (x's
  * shape, dtype and layout; required), the elementwise pass reads it -- three launches, as bb_bn_backward, and no
- * pass of the mask's own.  g is also the residual's gradient. */
+ * pass of the mask's own.  g is also the residual's gradient.  d_conv_ws non-NULL: a preceding convolution's
+ * weight-gradient reduction rides in the finalisation launch, as in bb_bn_backward_red. */
 int bb_bn_backward_res(const void* d_x, const void* d_dy, const void* d_y, int32_t dtype, int32_t nhwc, int32_t N,
                        int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias,
                        const float* d_save_mean, const float* d_save_invstd, double* d_ws, void* d_dx,
-                       float* d_dweight, float* d_dbias, float* d_dpre_bias, void* d_gres, void* stream);
+                       float* d_dweight, float* d_dbias, float* d_dpre_bias, void* d_gres, const float* d_conv_ws,
+                       int32_t conv_chunks, int32_t conv_cin, int32_t conv_cout, int32_t conv_w_layout,
+                       float* d_conv_dw, void* stream);
 
 /* The PPO minibatch loss (PPOAgent.update, ppo.py:362-401) with the masked
  * Categorical tail (network.py:173-180, 210-262), fused, forward and backward.
@@ -513,6 +517,11 @@ int bb_conv_in_forward(const float* d_x, int32_t x_nhwc, const float* d_w, int32
                        void* stream);
 int bb_conv_in_wgrad(const float* d_x, int32_t x_nhwc, const void* d_dy, int32_t N, float* d_ws, int32_t wl,
                      float* d_dw, void* stream);
+/* bb_conv_in_forward plus bb_conv3x3_prep_multi's weight images of the other layers (same table arguments) in one
+ * launch: both run at the start of the CNN's forward and are independent. */
+int bb_conv_in_forward_prep(const float* d_x, int32_t x_nhwc, const float* d_w, int32_t wl, int32_t N, void* d_y,
+                            int32_t count, const float* const* h_w, const int32_t* h_cin, const int32_t* h_cout,
+                            const int32_t* h_w_layout, void* const* h_wf, void* const* h_wd, void* stream);
 /* bb_linear_wgrad: a Linear's weight gradient dW = g^T x (g bf16 [rows][N], x bf16 [rows][K], dW bf16 [N][K],
  * all row-major; N and K multiples of 32, 16-byte aligned rows, rows <= 16384), f32 sums in a fixed order
  * rounded once (deterministic).  One launch: splits of 256 rows publish 32 x 32 partials to d_ws
