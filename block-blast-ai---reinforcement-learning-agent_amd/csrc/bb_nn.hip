@@ -485,8 +485,11 @@ Plan plan_for(int esz, int nhwc, int N, int C, int HW) {
 
 // Elementwise grids: NHWC threads keep V channels' coefficients in registers,
 // so they stride over >= 8 chunks each to amortise loading them.
+#ifndef BB_BN_APPLY_PT
+#define BB_BN_APPLY_PT 8
+#endif
 int grid_for_elems(int64_t chunks, int nhwc) {
-  const int64_t per_thread = nhwc ? 8 : 1;
+  const int64_t per_thread = nhwc ? BB_BN_APPLY_PT : 1;
   int64_t g = (chunks + kBnThreads * per_thread - 1) / (kBnThreads * per_thread);
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;

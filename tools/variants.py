@@ -87,6 +87,11 @@ VARIANTS = {
     "bnu4": ["-DBB_BN_UNROLL_BWD=4"],
     "bnf16": ["-DBB_BN_UNROLL_FWD=16"],
     "bnr1024": ["-DBB_BN_RBLOCKS=1024"],
+    "bnr256": ["-DBB_BN_RBLOCKS=256"],
+    # NHWC BatchNorm elementwise passes: 16-byte chunks per thread (shipped 8)
+    "bnpt2": ["-DBB_BN_APPLY_PT=2"],
+    "bnpt4": ["-DBB_BN_APPLY_PT=4"],
+    "bnpt16": ["-DBB_BN_APPLY_PT=16"],
     # LLVM AMDGPU scheduler strategies (shipped: max-ilp, runtime/build.py) and -O2
     "sdef": ["-mllvm", "-amdgpu-sched-strategy=default"],
     "smem": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
