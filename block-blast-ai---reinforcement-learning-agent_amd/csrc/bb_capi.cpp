@@ -1027,6 +1027,20 @@ extern "C" int bb_dropout_forward(void* d_y, int64_t n, float p, int64_t* d_rng,
   return BB_OK;
 }
 
+extern "C" int bb_linear_bgrad2(const void* d_dy, const void* d_dy2, int32_t split, const void* d_yd, int32_t rows,
+                                int32_t cols, float scale, void* d_g, void* d_db, float* d_ws, uint32_t* d_cnt,
+                                void* stream) {
+  if (!d_dy || !d_dy2 || !d_yd || !d_g || !d_db || !d_ws || !d_cnt)
+    return fail(nullptr, BB_ERR_ARG, "bb_linear_bgrad2: NULL argument");
+  if (rows <= 0 || cols <= 0) return fail(nullptr, BB_ERR_ARG, "bb_linear_bgrad2: rows and cols must be positive");
+  hipError_t st = launch_linear_bgrad(d_dy, d_yd, rows, cols, scale, d_g, d_db, d_ws, d_cnt, (hipStream_t)stream, d_dy2,
+                                      split);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_linear_bgrad2: split and cols - split multiples of 8, 16-byte aligned rows");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_bgrad2");
+  return BB_OK;
+}
+
 extern "C" int64_t bb_linear_bgrad_workspace_bytes(int32_t rows, int32_t cols) {
   return linear_bgrad_workspace_bytes(rows, cols);
 }
@@ -1088,13 +1102,13 @@ extern "C" int64_t bb_linear_wgrad_workspace_bytes(int32_t rows, int32_t N, int3
 
 extern "C" int32_t bb_linear_wgrad_counters(int32_t N, int32_t K) { return linear_wgrad_counters(N, K); }
 
-extern "C" int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, int32_t N, int32_t K, void* d_dw,
-                               float* d_ws, uint32_t* d_cnt, void* stream) {
+extern "C" int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, int32_t N, int32_t K, int32_t ldx,
+                               void* d_dw, float* d_ws, uint32_t* d_cnt, void* stream) {
   if (!d_g || !d_x || !d_dw || !d_ws || !d_cnt) return fail(nullptr, BB_ERR_ARG, "bb_linear_wgrad: NULL argument");
-  hipError_t st = launch_linear_wgrad(d_g, d_x, rows, N, K, d_dw, d_ws, d_cnt, (hipStream_t)stream);
+  hipError_t st = launch_linear_wgrad(d_g, d_x, rows, N, K, ldx, d_dw, d_ws, d_cnt, (hipStream_t)stream);
   if (st == hipErrorInvalidValue)
     return fail(nullptr, BB_ERR_ARG,
-                "bb_linear_wgrad: 0 < rows <= 16384, N and K multiples of 32, 16-byte aligned rows");
+                "bb_linear_wgrad: 0 < rows <= 16384, N and K multiples of 32, ldx >= K a multiple of 8, aligned rows");
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_wgrad");
   return BB_OK;
 }
@@ -1103,20 +1117,24 @@ extern "C" int64_t bb_linear_n1_workspace_bytes(int32_t rows, int32_t K) { retur
 
 extern "C" int32_t bb_linear_n1_counters(int32_t K) { return linear_n1_counters(K); }
 
-extern "C" int bb_linear_n1_forward(const void* d_x, const void* d_w, const void* d_b, int32_t rows, int32_t K, void* d_y,
-                                    void* stream) {
-  hipError_t st = launch_linear_n1_forward(d_x, d_w, d_b, rows, K, d_y, (hipStream_t)stream);
+extern "C" int bb_linear_n1_forward(const void* d_x, const void* d_w, const void* d_b, int32_t rows, int32_t K, int32_t ldx,
+                                    void* d_y, void* stream) {
+  hipError_t st = launch_linear_n1_forward(d_x, d_w, d_b, rows, K, ldx, d_y, (hipStream_t)stream);
   if (st == hipErrorInvalidValue)
-    return fail(nullptr, BB_ERR_ARG, "bb_linear_n1_forward: rows > 0, K a multiple of 8, x / w non-NULL and aligned");
+    return fail(nullptr, BB_ERR_ARG,
+                "bb_linear_n1_forward: rows > 0, K and ldx >= K multiples of 8, x / w non-NULL and aligned");
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_n1_forward");
   return BB_OK;
 }
 
 extern "C" int bb_linear_n1_backward(const void* d_gy, const void* d_x, const void* d_w, int32_t rows, int32_t K,
-                                     void* d_dx, void* d_dw, void* d_db, float* d_ws, uint32_t* d_cnt, void* stream) {
-  hipError_t st = launch_linear_n1_backward(d_gy, d_x, d_w, rows, K, d_dx, d_dw, d_db, d_ws, d_cnt, (hipStream_t)stream);
+                                     int32_t ldx, void* d_dx, void* d_dw, void* d_db, float* d_ws, uint32_t* d_cnt,
+                                     void* stream) {
+  hipError_t st =
+      launch_linear_n1_backward(d_gy, d_x, d_w, rows, K, ldx, d_dx, d_dw, d_db, d_ws, d_cnt, (hipStream_t)stream);
   if (st == hipErrorInvalidValue)
-    return fail(nullptr, BB_ERR_ARG, "bb_linear_n1_backward: rows > 0, K a multiple of 8, aligned non-NULL buffers");
+    return fail(nullptr, BB_ERR_ARG,
+                "bb_linear_n1_backward: rows > 0, K and ldx >= K multiples of 8, aligned non-NULL buffers");
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_n1_backward");
   return BB_OK;
 }

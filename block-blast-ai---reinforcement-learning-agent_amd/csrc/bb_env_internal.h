@@ -179,16 +179,16 @@ hipError_t launch_dropout_fwd(void* y, int64_t n, float p, int64_t* rng, hipStre
 int64_t linear_bgrad_workspace_bytes(int rows, int cols);
 int linear_bgrad_counters(int cols);
 hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int cols, float scale, void* g, void* db,
-                               float* part, uint32_t* cnt, hipStream_t s);
+                               float* part, uint32_t* cnt, hipStream_t s, const void* dy2 = nullptr, int split = 0);
 int64_t linear_n1_workspace_bytes(int rows, int K);
 int linear_n1_counters(int K);
-hipError_t launch_linear_n1_forward(const void* x, const void* w, const void* b, int rows, int K, void* y,
+hipError_t launch_linear_n1_forward(const void* x, const void* w, const void* b, int rows, int K, int ldx, void* y,
                                     hipStream_t s);
-hipError_t launch_linear_n1_backward(const void* gy, const void* x, const void* w, int rows, int K, void* dx, void* dw,
-                                     void* db, float* part, uint32_t* cnt, hipStream_t s);
+hipError_t launch_linear_n1_backward(const void* gy, const void* x, const void* w, int rows, int K, int ldx, void* dx,
+                                     void* dw, void* db, float* part, uint32_t* cnt, hipStream_t s);
 int64_t linear_wgrad_workspace_bytes(int rows, int N, int K);
 int linear_wgrad_counters(int N, int K);
-hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, int K, void* dw, float* part,
+hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, int K, int ldx, void* dw, float* part,
                                uint32_t* cnt, hipStream_t s);
 
 // Host helpers (bb_tables.cpp).

@@ -396,7 +396,8 @@ __global__ void __launch_bounds__(kBgradThreads) linear_bgrad_kernel(const uint1
                                                                       int cols, int chunk_rows, float scale,
                                                                       uint16_t* __restrict__ g,
                                                                       uint16_t* __restrict__ db, float* part,
-                                                                      uint32_t* cnt) {
+                                                                      uint32_t* cnt, const uint16_t* __restrict__ dy2,
+                                                                      int split) {
   constexpr int RL = kBgradThreads / kBgradCL;
   __shared__ float wsum[kBgradThreads / 64][kBgradCols];
   const int cl = threadIdx.x % kBgradCL, rl = threadIdx.x / kBgradCL;
@@ -407,10 +408,14 @@ __global__ void __launch_bounds__(kBgradThreads) linear_bgrad_kernel(const uint1
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (VEC) {
     if (c0 < cols) {
+      // dy2: columns split.. come from a second row-major source (two layers' gradients side by side)
+      const bool second = dy2 && c0 >= split;
+      const uint16_t* src = second ? dy2 + (c0 - split) : dy + c0;
+      const int lds = second ? cols - split : (dy2 ? split : cols);
 #pragma unroll 4
       for (int r = r0 + rl; r < r1; r += RL) {
         const int64_t o = (int64_t)r * cols + c0;
-        const uint4 h = *reinterpret_cast<const uint4*>(dy + o);
+        const uint4 h = *reinterpret_cast<const uint4*>(src + (int64_t)r * lds);
         uint32_t w[4] = {h.x, h.y, h.z, h.w};
         if (yd) {
           const uint4 m = *reinterpret_cast<const uint4*>(yd + o);
@@ -507,7 +512,8 @@ __device__ __forceinline__ s16x4 tr_read(const uint16_t* lds) {
 
 __global__ void __launch_bounds__(256) linear_wgrad_kernel(const uint16_t* __restrict__ g,
                                                            const uint16_t* __restrict__ x, int rows, int N, int K,
-                                                           uint16_t* __restrict__ dw, float* part, uint32_t* cnt) {
+                                                           int ldx, uint16_t* __restrict__ dw, float* part,
+                                                           uint32_t* cnt) {
   __shared__ __attribute__((aligned(16))) uint16_t gs[kWgSplit][kWgT];
   __shared__ __attribute__((aligned(16))) uint16_t xs[kWgSplit][kWgT];
   __shared__ float red[4][kWgT * kWgT];
@@ -522,7 +528,7 @@ __global__ void __launch_bounds__(256) linear_wgrad_kernel(const uint16_t* __res
       const int r = r0 + lr + 64 * u;
       if (r < rows) {
         rg[u] = *reinterpret_cast<const uint4*>(g + (int64_t)r * N + n0 + lp);
-        rx[u] = *reinterpret_cast<const uint4*>(x + (int64_t)r * K + k0 + lp);
+        rx[u] = *reinterpret_cast<const uint4*>(x + (int64_t)r * ldx + k0 + lp);
       } else {
         rg[u] = make_uint4(0u, 0u, 0u, 0u);
         rx[u] = rg[u];
@@ -614,13 +620,13 @@ constexpr int kN1Slots = kBgradCols + 1;
 
 __global__ void __launch_bounds__(256) linear_n1_fwd_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ w,
-                                                            const uint16_t* __restrict__ b, int rows, int K,
+                                                            const uint16_t* __restrict__ b, int rows, int K, int ldx,
                                                             uint16_t* __restrict__ y) {
   const int r = blockIdx.x * kN1Rows + (threadIdx.x >> 4), l = threadIdx.x & 15;
   float s = 0.f;
   if (r < rows)
     for (int k = 8 * l; k < K; k += 128) {
-      const uint4 xv = *reinterpret_cast<const uint4*>(x + (int64_t)r * K + k);
+      const uint4 xv = *reinterpret_cast<const uint4*>(x + (int64_t)r * ldx + k);
       const uint4 wv = *reinterpret_cast<const uint4*>(w + k);
       const uint32_t xa[4] = {xv.x, xv.y, xv.z, xv.w}, wa[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
@@ -637,7 +643,7 @@ __global__ void __launch_bounds__(256) linear_n1_fwd_kernel(const uint16_t* __re
 __global__ void __launch_bounds__(256) linear_n1_bwd_kernel(const uint16_t* __restrict__ gy,
                                                             const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ w, int rows, int K,
-                                                            int chunk_rows, uint16_t* __restrict__ dx,
+                                                            int ldx, int chunk_rows, uint16_t* __restrict__ dx,
                                                             uint16_t* __restrict__ dw, uint16_t* __restrict__ db,
                                                             float* part, uint32_t* cnt) {
   __shared__ float wsum[4][kN1Slots];
@@ -664,7 +670,7 @@ __global__ void __launch_bounds__(256) linear_n1_bwd_kernel(const uint16_t* __re
     acc[8] += gv;
     if (live) {
       const int64_t o = (int64_t)r * K + c0;
-      const uint4 h = *reinterpret_cast<const uint4*>(x + o);
+      const uint4 h = *reinterpret_cast<const uint4*>(x + (int64_t)r * ldx + c0);
       const uint32_t xa[4] = {h.x, h.y, h.z, h.w};
       uint32_t d[4];
 #pragma unroll
@@ -820,20 +826,23 @@ int64_t linear_bgrad_workspace_bytes(int rows, int cols) {
 int linear_bgrad_counters(int cols) { return cols > 0 ? (cols + kBgradCols - 1) / kBgradCols : -1; }
 
 hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int cols, float scale, void* g, void* db,
-                               float* part, uint32_t* cnt, hipStream_t s) {
+                               float* part, uint32_t* cnt, hipStream_t s, const void* dy2, int split) {
   if (rows <= 0 || cols <= 0 || !dy || !db || (yd && !g) || !part || !cnt) return hipErrorInvalidValue;
   const bool vec = cols % 8 == 0 &&
-                   ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(yd) | reinterpret_cast<uintptr_t>(g)) &
-                    15) == 0;
+                   ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(yd) | reinterpret_cast<uintptr_t>(g) |
+                     reinterpret_cast<uintptr_t>(dy2)) & 15) == 0;
+  if (dy2 && (!vec || split <= 0 || split >= cols || split % 8 || (cols - split) % 8)) return hipErrorInvalidValue;
   const int nsplit = bgrad_split(rows);
   const int chunk = (rows + nsplit - 1) / nsplit;
   const dim3 grid((cols + kBgradCols - 1) / kBgradCols, nsplit);
   if (vec)
     hipLaunchKernelGGL(linear_bgrad_kernel<true>, grid, dim3(kBgradThreads), 0, s, (const uint16_t*)dy,
-                       (const uint16_t*)yd, rows, cols, chunk, scale, (uint16_t*)g, (uint16_t*)db, part, cnt);
+                       (const uint16_t*)yd, rows, cols, chunk, scale, (uint16_t*)g, (uint16_t*)db, part, cnt,
+                       (const uint16_t*)dy2, split);
   else
     hipLaunchKernelGGL(linear_bgrad_kernel<false>, grid, dim3(kBgradThreads), 0, s, (const uint16_t*)dy,
-                       (const uint16_t*)yd, rows, cols, chunk, scale, (uint16_t*)g, (uint16_t*)db, part, cnt);
+                       (const uint16_t*)yd, rows, cols, chunk, scale, (uint16_t*)g, (uint16_t*)db, part, cnt,
+                       (const uint16_t*)nullptr, 0);
   return hipGetLastError();
 }
 
@@ -845,14 +854,14 @@ int64_t linear_wgrad_workspace_bytes(int rows, int N, int K) {
 
 int linear_wgrad_counters(int N, int K) { return (N % kWgT || K % kWgT) ? -1 : (N / kWgT) * (K / kWgT); }
 
-hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, int K, void* dw, float* part,
+hipError_t launch_linear_wgrad(const void* g, const void* x, int rows, int N, int K, int ldx, void* dw, float* part,
                                uint32_t* cnt, hipStream_t s) {
-  if (linear_wgrad_workspace_bytes(rows, N, K) < 0 || !g || !x || !dw || !part || !cnt ||
+  if (linear_wgrad_workspace_bytes(rows, N, K) < 0 || !g || !x || !dw || !part || !cnt || ldx < K || ldx % 8 ||
       ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(x)) & 15))
     return hipErrorInvalidValue;
   const int nsplit = (rows + kWgSplit - 1) / kWgSplit;
   hipLaunchKernelGGL(linear_wgrad_kernel, dim3(K / kWgT, N / kWgT, nsplit), dim3(256), 0, s, (const uint16_t*)g,
-                     (const uint16_t*)x, rows, N, K, (uint16_t*)dw, part, cnt);
+                     (const uint16_t*)x, rows, N, K, ldx, (uint16_t*)dw, part, cnt);
   return hipGetLastError();
 }
 
@@ -863,25 +872,25 @@ int64_t linear_n1_workspace_bytes(int rows, int K) {
 
 int linear_n1_counters(int K) { return K > 0 ? (K + kBgradCols - 1) / kBgradCols : -1; }
 
-hipError_t launch_linear_n1_forward(const void* x, const void* w, const void* b, int rows, int K, void* y,
+hipError_t launch_linear_n1_forward(const void* x, const void* w, const void* b, int rows, int K, int ldx, void* y,
                                     hipStream_t s) {
-  if (rows <= 0 || K <= 0 || K % 8 || !x || !w || !y ||
+  if (rows <= 0 || K <= 0 || K % 8 || ldx < K || ldx % 8 || !x || !w || !y ||
       ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(linear_n1_fwd_kernel, dim3((rows + kN1Rows - 1) / kN1Rows), dim3(256), 0, s, (const uint16_t*)x,
-                     (const uint16_t*)w, (const uint16_t*)b, rows, K, (uint16_t*)y);
+                     (const uint16_t*)w, (const uint16_t*)b, rows, K, ldx, (uint16_t*)y);
   return hipGetLastError();
 }
 
-hipError_t launch_linear_n1_backward(const void* gy, const void* x, const void* w, int rows, int K, void* dx, void* dw,
-                                     void* db, float* part, uint32_t* cnt, hipStream_t s) {
-  if (linear_n1_workspace_bytes(rows, K) < 0 || !gy || !x || !w || !dx || !dw || !part || !cnt ||
+hipError_t launch_linear_n1_backward(const void* gy, const void* x, const void* w, int rows, int K, int ldx, void* dx,
+                                     void* dw, void* db, float* part, uint32_t* cnt, hipStream_t s) {
+  if (linear_n1_workspace_bytes(rows, K) < 0 || ldx < K || ldx % 8 || !gy || !x || !w || !dx || !dw || !part || !cnt ||
       ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dx)) & 15))
     return hipErrorInvalidValue;
   const int nsplit = bgrad_split(rows);
   const int chunk = (rows + nsplit - 1) / nsplit;
   hipLaunchKernelGGL(linear_n1_bwd_kernel, dim3((K + kBgradCols - 1) / kBgradCols, nsplit), dim3(256), 0, s,
-                     (const uint16_t*)gy, (const uint16_t*)x, (const uint16_t*)w, rows, K, chunk, (uint16_t*)dx,
+                     (const uint16_t*)gy, (const uint16_t*)x, (const uint16_t*)w, rows, K, ldx, chunk, (uint16_t*)dx,
                      (uint16_t*)dw, (uint16_t*)db, part, cnt);
   return hipGetLastError();
 }

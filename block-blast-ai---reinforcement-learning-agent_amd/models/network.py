@@ -61,6 +61,7 @@ NHWC_FLATTEN = os.environ.get("BB_NHWC_FLATTEN", "1") != "0"  # channels_last tr
 FUSED_CASTS = os.environ.get("BB_FUSED_CASTS", "1") != "0"  # bf16 Linear weights/biases cast in one launch each way
 CAST_PERM_ROW_MAX = 8192  # bb_cast_multi's permuted-row limit (perm_c * perm_hw, include/bbvec.h)
 LINEAR_RELU = os.environ.get("BB_LINEAR_RELU", "1") != "0"  # bf16 Linear -> ReLU: the ReLU in the GEMM epilogue
+HEADS_FUSED = os.environ.get("BB_HEADS_FUSED", "1") != "0"  # both heads' first layers as one GEMM (HeadsFunction)
 PREP_MULTI = os.environ.get("BB_PREP_MULTI", "1") != "0"  # the HIP convs' weight images in one launch
 RES_FUSED = os.environ.get("BB_RES_FUSED", "1") != "0"  # ResidualBlock's bn2 + identity + relu in one BatchNorm pass
 # ... and the identity path's input gradient added in conv1's data-gradient store pass (no add kernel)
@@ -272,25 +273,45 @@ class BlockBlastNetwork(nn.Module):
         if perm0 is not None and perm0[0] * perm0[1] > CAST_PERM_ROW_MAX:
             return None  # bb_cast_multi permutes one row per workgroup through LDS: autocast's path instead
         lins = self._linears()
-        params, perms, slots = [], [], []
-        for m in lins:
-            perm = perm0 if (perm0 is not None and len(self.fc_encoder) and m is self.fc_encoder[0]) else (0, 0)
-            params.append(m.weight)
-            perms.append(perm)
-            if m.bias is not None:
-                params.append(m.bias)
-                perms.append((0, 0))
-            slots.append(m.bias is not None)
+        entries = [(m, kind) for m in lins for kind in (("w", "b") if m.bias is not None else ("w",))]
+        heads = self._head_pair()
+        if heads is not None:  # the heads' first weights, then their biases, back to back (HeadsFunction)
+            p0, v0 = heads
+            tail = [(p0, "w"), (v0, "w"), (p0, "b"), (v0, "b")]
+            entries = [e for e in entries if e not in tail] + tail
+        params, perms = [], []
+        for m, kind in entries:
+            first = perm0 is not None and len(self.fc_encoder) and m is self.fc_encoder[0] and kind == "w"
+            params.append(m.weight if kind == "w" else m.bias)
+            perms.append(perm0 if first else (0, 0))
         if not params or len(params) > 48 or any(p.dtype != torch.float32 or not p.is_contiguous() for p in params):
             return None
         from runtime.kernels import LinearCastFunction
 
-        outs = list(LinearCastFunction.apply(tuple(perms), *params))
-        sh, k = {}, 0
-        for m, has_b in zip(lins, slots):
-            sh[m] = (outs[k], outs[k + 1] if has_b else None)
-            k += 2 if has_b else 1
-        return sh
+        outs = dict(zip(entries, LinearCastFunction.apply(tuple(perms), *params)))
+        return {m: (outs[(m, "w")], outs.get((m, "b"))) for m in lins}
+
+    def _head_pair(self):
+        """(policy_head[0], value_head[0]) when both heads are Linear -> ReLU -> Linear with biases (the
+        reference's heads) and HeadsFunction may run them, else None."""
+        p, v = list(self.policy_head), list(self.value_head)
+        shape = lambda s: (len(s) == 3 and isinstance(s[0], nn.Linear) and isinstance(s[1], nn.ReLU)
+                           and isinstance(s[2], nn.Linear) and s[0].bias is not None and s[2].bias is not None)
+        if HEADS_FUSED and LINEAR_RELU and shape(p) and shape(v) and v[2].out_features == 1:
+            return p[0], v[0]
+        return None
+
+    def _heads(self, h: torch.Tensor, sh):
+        """(logits, value (B, 1)) from HeadsFunction when it applies, else None."""
+        pair = self._head_pair() if sh is not None and h.dim() == 2 else None
+        if pair is None:
+            return None
+        from runtime import kernels as K
+
+        args = (*sh[pair[0]], *sh[pair[1]], *sh[self.policy_head[2]], *sh[self.value_head[2]])
+        if not K.heads_ok(h, *args):
+            return None
+        return K.HeadsFunction.apply(h, *args)
 
     def _dropout_after(self, mods, i: int, z: torch.Tensor):
         """(p, rng) when mods[i] is an nn.Dropout the bf16 Linear tail applies itself (bb_dropout_forward),
@@ -422,6 +443,9 @@ class BlockBlastNetwork(nn.Module):
     def raw(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Unmasked logits (B, 192) and value (B,) from the stacked input."""
         h, sh = self._trunk(x)
+        heads = self._heads(h, sh)
+        if heads is not None:
+            return heads[0], heads[1].squeeze(-1)
         return self._run(self.policy_head, h, sh), self._run(self.value_head, h, sh).squeeze(-1)
 
     @staticmethod

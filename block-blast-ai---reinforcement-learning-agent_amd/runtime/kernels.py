@@ -820,6 +820,12 @@ def _bgrad_ok(t: torch.Tensor) -> bool:
     return LINEAR_TAIL and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous()
 
 
+def _rows_ok(t: torch.Tensor) -> bool:
+    """A bf16 matrix whose rows are contiguous and 16-byte aligned (a column slice of a wider one allowed)."""
+    return (LINEAR_TAIL and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1
+            and t.stride(0) >= t.shape[1] and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
+
+
 _bgrad_cnt = {}  # (device, stream) -> zeroed uint32 counters of bb_linear_bgrad (re-armed by every launch)
 _BGRAD_CNT = 4096
 
@@ -853,6 +859,25 @@ def linear_bgrad(gy: torch.Tensor, yd: Optional[torch.Tensor], scale: float = 1.
     return g, db
 
 
+def linear_bgrad2(gy: torch.Tensor, gy2: torch.Tensor, yd: torch.Tensor):
+    """bb_linear_bgrad2: (g, db) of bb_linear_bgrad over [gy | gy2] (two layers' output gradients side by
+    side, yd the two layers' joint output), without concatenating them."""
+    rows, split = gy.shape
+    cols = yd.shape[1]
+    if not (_bgrad_ok(gy) and _bgrad_ok(gy2) and _bgrad_ok(yd) and gy2.shape == (rows, cols - split)
+            and yd.shape[0] == rows):
+        raise L.BBNativeError("linear_bgrad2: contiguous bf16 [rows][split], [rows][cols - split], [rows][cols]")
+    dev = gy.device
+    lib = L.load()
+    g = torch.empty_like(yd)
+    db = torch.empty(cols, dtype=gy.dtype, device=dev)
+    ws = torch.empty((lib.bb_linear_bgrad_workspace_bytes(rows, cols) + 3) // 4, dtype=torch.float32, device=dev)
+    cnt = _bgrad_counters(dev, lib.bb_linear_bgrad_counters(cols))
+    L.check(lib.bb_linear_bgrad2(_p(gy), _p(gy2), split, _p(yd), rows, cols, 1.0, _p(g), _p(db), _p(ws), _p(cnt),
+                                 _s(dev)), "bb_linear_bgrad2")
+    return g, db
+
+
 WGRAD_MAX = 512 * 512  # bb_linear_wgrad for weights up to this size (the 8,192-column first FC stays hipBLASLt's)
 
 
@@ -860,14 +885,15 @@ def linear_wgrad(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """g^T x (autograd's weight gradient of F.linear) on bb_linear_wgrad when the shapes fit, else torch's mm."""
     rows, n = g.shape
     k = x.shape[1]
-    if (_bgrad_ok(g) and _bgrad_ok(x) and x.shape[0] == rows and n % 32 == 0 and k % 32 == 0 and n * k <= WGRAD_MAX
+    if (_bgrad_ok(g) and _rows_ok(x) and x.shape[0] == rows and n % 32 == 0 and k % 32 == 0 and n * k <= WGRAD_MAX
             and 0 < rows <= 16384):
         lib = L.load()
         dev = g.device
         dw = torch.empty((n, k), dtype=g.dtype, device=dev)
         ws = torch.empty((lib.bb_linear_wgrad_workspace_bytes(rows, n, k) + 3) // 4, dtype=torch.float32, device=dev)
         cnt = _bgrad_counters(dev, lib.bb_linear_wgrad_counters(n, k))
-        L.check(lib.bb_linear_wgrad(_p(g), _p(x), rows, n, k, _p(dw), _p(ws), _p(cnt), _s(dev)), "bb_linear_wgrad")
+        L.check(lib.bb_linear_wgrad(_p(g), _p(x), rows, n, k, x.stride(0), _p(dw), _p(ws), _p(cnt), _s(dev)),
+                "bb_linear_wgrad")
         return dw
     return g.t().mm(x)
 
@@ -938,8 +964,8 @@ class LinearN1Function(torch.autograd.Function):
         _need_cuda(x, weight)
         rows, k = x.shape
         y = torch.empty((rows, 1), dtype=x.dtype, device=x.device)
-        L.check(L.load().bb_linear_n1_forward(_p(x), _p(weight), _p(bias), rows, k, _p(y), _s(x.device)),
-                "bb_linear_n1_forward")
+        L.check(L.load().bb_linear_n1_forward(_p(x), _p(weight), _p(bias), rows, k, x.stride(0), _p(y),
+                                              _s(x.device)), "bb_linear_n1_forward")
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         return y
@@ -951,14 +977,86 @@ class LinearN1Function(torch.autograd.Function):
         dev = x.device
         lib = L.load()
         gy = gy.contiguous()
-        dx = torch.empty_like(x)
-        dw = torch.empty_like(weight)
-        db = torch.empty(1, dtype=x.dtype, device=dev) if ctx.has_bias else None
-        ws = torch.empty((lib.bb_linear_n1_workspace_bytes(rows, k) + 3) // 4, dtype=torch.float32, device=dev)
-        cnt = _bgrad_counters(dev, lib.bb_linear_n1_counters(k))
-        L.check(lib.bb_linear_n1_backward(_p(gy), _p(x), _p(weight), rows, k, _p(dx), _p(dw), _p(db), _p(ws), _p(cnt),
-                                          _s(dev)), "bb_linear_n1_backward")
+        dx, dw, db = _n1_backward(gy, x, weight, ctx.has_bias)
         return dx, dw, db
+
+
+def _n1_backward(gy, x, weight, has_bias: bool):
+    """(dx, dW, db) of bb_linear_n1_backward; x may be a column slice (row stride x.stride(0))."""
+    rows, k = x.shape
+    dev = x.device
+    lib = L.load()
+    dx = torch.empty((rows, k), dtype=x.dtype, device=dev)
+    dw = torch.empty_like(weight)
+    db = torch.empty(1, dtype=x.dtype, device=dev) if has_bias else None
+    ws = torch.empty((lib.bb_linear_n1_workspace_bytes(rows, k) + 3) // 4, dtype=torch.float32, device=dev)
+    cnt = _bgrad_counters(dev, lib.bb_linear_n1_counters(k))
+    L.check(lib.bb_linear_n1_backward(_p(gy), _p(x), _p(weight), rows, k, x.stride(0), _p(dx), _p(dw), _p(db), _p(ws),
+                                      _p(cnt), _s(dev)), "bb_linear_n1_backward")
+    return dx, dw, db
+
+
+class HeadsFunction(torch.autograd.Function):
+    """The policy and value heads (src/models/network.py:106-120 of the reference: Linear(F, 256) -> ReLU -> Linear(256, 192)
+    and Linear(F, 128) -> ReLU -> Linear(128, 1)) on the same features h, their first layers as ONE GEMM with
+    the ReLU in its epilogue: wp0 / wv0 and bp0 / bv0 must lie back to back in memory (the Linear shadows of
+    network.py allocate them so), read as one [384][F] weight and [384] bias.  Then the policy's last layer
+    on hipBLASLt (a column slice of the joint output) and the value's on bb_linear_n1_forward.  Backward:
+    bb_linear_bgrad (policy bias), bb_linear_wgrad, one GEMM for the policy's hidden gradient,
+    bb_linear_n1_backward, bb_linear_bgrad2 (both hidden layers' ReLU masks and biases in one pass), then one
+    GEMM for dh (both heads' input gradients summed inside it) and one bb_linear_wgrad for both first-layer
+    weights: 7 launches for the 11 the separate layers take (and 3 for 4 forward)."""
+
+    @staticmethod
+    def forward(ctx, h, wp0, bp0, wv0, bv0, wp2, bp2, wv2, bv2):
+        _need_cuda(h, wp0)
+        n0, k = wp0.shape
+        n = n0 + wv0.shape[0]
+        w_cat = wp0.as_strided((n, k), (k, 1))
+        b_cat = bp0.as_strided((n,), (1,))
+        y = torch._addmm_activation(b_cat, h, w_cat.t())
+        logits = torch.addmm(bp2, y[:, :n0], wp2.t())
+        yv = y[:, n0:]
+        value = torch.empty((h.shape[0], 1), dtype=h.dtype, device=h.device)
+        L.check(L.load().bb_linear_n1_forward(_p(yv), _p(wv2), _p(bv2), h.shape[0], n - n0, n, _p(value),
+                                              _s(h.device)), "bb_linear_n1_forward")
+        ctx.save_for_backward(h, wp0, wp2, wv2, y)
+        ctx.n0 = n0
+        ctx.has_bv2 = bv2 is not None
+        return logits, value
+
+    @staticmethod
+    def backward(ctx, glog, gval):
+        h, wp0, wp2, wv2, y = ctx.saved_tensors
+        n0 = ctx.n0
+        n, k = y.shape[1], h.shape[1]
+        glog = glog.contiguous()
+        gval = gval.contiguous()
+        dbp2 = linear_bgrad(glog, None)[1]
+        dwp2 = linear_wgrad(glog, y[:, :n0])
+        dyp = glog.mm(wp2)
+        dyv, dwv2, dbv2 = _n1_backward(gval, y[:, n0:], wv2, ctx.has_bv2)
+        g, db_cat = linear_bgrad2(dyp, dyv, y)
+        dh = g.mm(wp0.as_strided((n, k), (k, 1))) if ctx.needs_input_grad[0] else None
+        dw_cat = linear_wgrad(g, h)
+        return dh, dw_cat[:n0], db_cat[:n0], dw_cat[n0:], db_cat[n0:], dwp2, dbp2, dwv2, dbv2
+
+
+def heads_ok(h: torch.Tensor, wp0, bp0, wv0, bv0, wp2, bp2, wv2, bv2) -> bool:
+    """HeadsFunction applies: bf16 features and shadows, the first layers' weights and biases adjacent."""
+    if not (_bgrad_ok(h) and h.shape[0] > 0 and bp0 is not None and bv0 is not None and bp2 is not None):
+        return False
+    ts = (wp0, bp0, wv0, bv0, wp2, bp2, wv2)
+    if any(t.dtype != torch.bfloat16 or not t.is_contiguous() or not t.is_cuda for t in ts):
+        return False
+    n0, k = wp0.shape
+    nv = wv0.shape[0]
+    return (wv0.shape[1] == k == h.shape[1] and bp0.numel() == n0 and bv0.numel() == nv
+            and wv0.untyped_storage().data_ptr() == wp0.untyped_storage().data_ptr()
+            and bv0.untyped_storage().data_ptr() == bp0.untyped_storage().data_ptr()
+            and wv0.data_ptr() == wp0.data_ptr() + 2 * n0 * k and bv0.data_ptr() == bp0.data_ptr() + 2 * n0
+            and n0 % 32 == 0 and nv % 32 == 0 and k % 32 == 0 and wp2.shape[1] == n0 and wp2.shape[0] % 32 == 0
+            and tuple(wv2.shape) == (1, nv) and (n0 + nv) * k <= WGRAD_MAX and h.shape[0] <= 16384)
 
 
 def linear_n1_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -979,7 +1077,14 @@ class LinearCastFunction(torch.autograd.Function):
         for p in params:
             if p.dtype != torch.float32 or not p.is_contiguous():
                 raise L.BBNativeError("LinearCastFunction: contiguous f32 parameters only")
-        outs = [torch.empty(p.shape, dtype=torch.bfloat16, device=p.device) for p in params]
+        # one buffer, each slot 256-byte aligned: consecutive parameters whose sizes are multiples of 128
+        # elements lie back to back (HeadsFunction reads two heads' layers as one)
+        offs, tot = [], 0
+        for p in params:
+            offs.append(tot)
+            tot += (p.numel() + 127) // 128 * 128
+        buf = torch.empty(tot, dtype=torch.bfloat16, device=params[0].device)
+        outs = [buf[o:o + p.numel()].view(p.shape) for o, p in zip(offs, params)]
         cast_multi(0, params, outs, perms)
         ctx.perms = perms
         ctx.set_materialize_grads(False)  # an unused output leaves its parameter's .grad None, as autocast does

@@ -181,14 +181,15 @@ SIGNATURES = {
     "bb_conv_in_forward_prep": (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "bb_linear_n1_workspace_bytes": (C.c_int64, [_I32, _I32]),
     "bb_linear_n1_counters": (C.c_int32, [_I32]),
-    "bb_linear_n1_forward": (C.c_int, [_P, _P, _P, _I32, _I32, _P, _P]),
-    "bb_linear_n1_backward": (C.c_int, [_P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "bb_linear_n1_forward": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P]),
+    "bb_linear_n1_backward": (C.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "bb_linear_wgrad_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
     "bb_linear_wgrad_counters": (C.c_int32, [_I32, _I32]),
-    "bb_linear_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "bb_linear_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     "bb_linear_bgrad_workspace_bytes": (C.c_int64, [_I32, _I32]),
     "bb_linear_bgrad_counters": (C.c_int32, [_I32]),
     "bb_linear_bgrad": (C.c_int, [_P, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),
+    "bb_linear_bgrad2": (C.c_int, [_P, _P, _I32, _P, _I32, _I32, _F, _P, _P, _P, _P, _P]),
 }
 
 # the env entry points, which the host backend (libbbvec_host.so) exports too

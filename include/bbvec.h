@@ -42,7 +42,7 @@ extern "C" {
                                  bb_conv_in_forward / _wgrad; bb_bn_backward_res; bb_ppo_loss_fused and the
                                  loss forward's d_cnt (one launch, the statistics finalised in it);
                                  bb_conv3x3_wgrad_partial / _reduce / _chunks, bb_bn_backward_red,
-                                 bb_conv_in_forward_prep */
+                                 bb_conv_in_forward_prep, bb_linear_bgrad2 */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -522,32 +522,37 @@ int bb_conv_in_wgrad(const float* d_x, int32_t x_nhwc, const void* d_dy, int32_t
 int bb_conv_in_forward_prep(const float* d_x, int32_t x_nhwc, const float* d_w, int32_t wl, int32_t N, void* d_y,
                             int32_t count, const float* const* h_w, const int32_t* h_cin, const int32_t* h_cout,
                             const int32_t* h_w_layout, void* const* h_wf, void* const* h_wd, void* stream);
-/* bb_linear_wgrad: a Linear's weight gradient dW = g^T x (g bf16 [rows][N], x bf16 [rows][K], dW bf16 [N][K],
- * all row-major; N and K multiples of 32, 16-byte aligned rows, rows <= 16384), f32 sums in a fixed order
+/* bb_linear_wgrad: a Linear's weight gradient dW = g^T x (g bf16 [rows][N], x bf16 [rows][K] with row stride
+ * ldx >= K a multiple of 8, dW bf16 [N][K], all row-major; N and K multiples of 32, 16-byte aligned rows, rows <= 16384), f32 sums in a fixed order
  * rounded once (deterministic).  One launch: splits of 256 rows publish 32 x 32 partials to d_ws
  * (bb_linear_wgrad_workspace_bytes(rows, N, K) bytes) and the last split of a tile adds them; d_cnt: the
  * bb_linear_wgrad_counters(N, K) uint32 counters, zero before and after each launch (as bb_linear_bgrad's,
  * and the same counter block may serve both on one stream). */
 /* bb_linear_n1_forward / _backward: a bf16 Linear with one output (the value head's Linear(128, 1)), x bf16
- * [rows][K], w bf16 [K], b bf16 [1] (NULL: none), K a multiple of 8, 16-byte aligned.  Forward: y[r] =
- * bf16(sum_k x[r][k] w[k] + b), f32 sums.  Backward: dx[r][k] = bf16(gy[r] w[k]), dW[k] = sum_r gy[r] x[r][k],
+ * [rows][K] with row stride ldx (>= K, a multiple of 8), w bf16 [K], b bf16 [1] (NULL: none), K a multiple of
+ * 8, 16-byte aligned.  Forward: y[r] = bf16(sum_k x[r][k] w[k] + b), f32 sums.  Backward: dx[r][k] = bf16(gy[r] w[k]), dW[k] = sum_r gy[r] x[r][k],
  * db = sum_r gy[r] (d_db NULL: skipped), f32 sums in a fixed order rounded to bf16; row chunks publish
  * partials to d_ws (bb_linear_n1_workspace_bytes(rows, K) bytes) with bb_linear_n1_counters(K) zeroed
  * counters in d_cnt (as bb_linear_bgrad).  One launch each. */
 int64_t bb_linear_n1_workspace_bytes(int32_t rows, int32_t K);
 int32_t bb_linear_n1_counters(int32_t K);
-int bb_linear_n1_forward(const void* d_x, const void* d_w, const void* d_b, int32_t rows, int32_t K, void* d_y,
-                         void* stream);
-int bb_linear_n1_backward(const void* d_gy, const void* d_x, const void* d_w, int32_t rows, int32_t K, void* d_dx,
-                          void* d_dw, void* d_db, float* d_ws, uint32_t* d_cnt, void* stream);
+int bb_linear_n1_forward(const void* d_x, const void* d_w, const void* d_b, int32_t rows, int32_t K, int32_t ldx,
+                         void* d_y, void* stream);
+int bb_linear_n1_backward(const void* d_gy, const void* d_x, const void* d_w, int32_t rows, int32_t K, int32_t ldx,
+                          void* d_dx, void* d_dw, void* d_db, float* d_ws, uint32_t* d_cnt, void* stream);
 int64_t bb_linear_wgrad_workspace_bytes(int32_t rows, int32_t N, int32_t K);
 int32_t bb_linear_wgrad_counters(int32_t N, int32_t K);
-int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, int32_t N, int32_t K, void* d_dw, float* d_ws,
-                    uint32_t* d_cnt, void* stream);
+int bb_linear_wgrad(const void* d_g, const void* d_x, int32_t rows, int32_t N, int32_t K, int32_t ldx, void* d_dw,
+                    float* d_ws, uint32_t* d_cnt, void* stream);
 int64_t bb_linear_bgrad_workspace_bytes(int32_t rows, int32_t cols);
 int32_t bb_linear_bgrad_counters(int32_t cols);
 int bb_linear_bgrad(const void* d_dy, const void* d_yd, int32_t rows, int32_t cols, float scale, void* d_g,
                     void* d_db, float* d_ws, uint32_t* d_cnt, void* stream);
+/* bb_linear_bgrad over two layers' output gradients side by side (ABI 8): columns [0, split) of dy come from d_dy
+ * ([rows][split]), columns [split, cols) from d_dy2 ([rows][cols - split]); d_yd, d_g are [rows][cols] (the
+ * policy and value heads' first layers as one GEMM). */
+int bb_linear_bgrad2(const void* d_dy, const void* d_dy2, int32_t split, const void* d_yd, int32_t rows, int32_t cols,
+                     float scale, void* d_g, void* d_db, float* d_ws, uint32_t* d_cnt, void* stream);
 
 #ifdef __cplusplus
 }

@@ -201,6 +201,7 @@ def test_network_linear_tail_equals_torch_tails(cuda, monkeypatch):
     x = (torch.rand((512, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
     state0 = {k: v.clone() for k, v in net.state_dict().items()}
     res = {}
+    monkeypatch.setattr(N, "HEADS_FUSED", False)  # the joint heads GEMM is test_heads_function_*'s
     for tail in (True, False):
         monkeypatch.setattr(K, "LINEAR_TAIL", tail)
         net.load_state_dict(state0)
@@ -213,6 +214,90 @@ def test_network_linear_tail_equals_torch_tails(cuda, monkeypatch):
     # the value head's one-output layer sums in another order (bb_linear_n1_forward): one bf16 rounding apart
     assert torch.allclose(res[True][1], res[False][1], rtol=2.0 ** -7, atol=1e-6)
     for n, gr in res[True][2].items():
+        ref = res[False][2][n]
+        rel = float((gr - ref).norm() / ref.norm().clamp_min(1e-30))
+        assert rel < 1e-2, (n, rel)
+
+
+def _heads_params(cuda, k, seed):
+    """bf16 head weights with wp0 / wv0 and bp0 / bv0 back to back (as the network's shadow buffer)."""
+    g0 = torch.Generator(device=cuda).manual_seed(seed)
+    w_cat = _bf(torch.randn((384, k), device=cuda, generator=g0) * 0.05)
+    b_cat = _bf(torch.randn(384, device=cuda, generator=g0) * 0.1)
+    wp2 = _bf(torch.randn((192, 256), device=cuda, generator=g0) * 0.05)
+    bp2 = _bf(torch.randn(192, device=cuda, generator=g0) * 0.1)
+    wv2 = _bf(torch.randn((1, 128), device=cuda, generator=g0) * 0.1)
+    bv2 = _bf(torch.randn(1, device=cuda, generator=g0))
+    return w_cat, b_cat, wp2, bp2, wv2, bv2
+
+
+@pytest.mark.parametrize("rows,k", [(2048, 512), (1000, 256), (37, 64)])
+def test_heads_function_matches_fp64(cuda, rows, k):
+    """HeadsFunction (both heads' first layers as one GEMM + ReLU epilogue, the policy's last layer on a column
+    slice, the value's on bb_linear_n1_forward; backward through bb_linear_bgrad2 and one dh GEMM): every
+    stage within one bf16 rounding of fp64 on the same bf16 operands, the ReLU-masked hidden gradient exact."""
+    from runtime import kernels as K
+
+    w_cat, b_cat, wp2, bp2, wv2, bv2 = _heads_params(cuda, k, rows + k)
+    g0 = torch.Generator(device=cuda).manual_seed(k)
+    h0 = _bf(torch.randn((rows, k), device=cuda, generator=g0)).clamp_min(0)
+    glog = _bf(torch.randn((rows, 192), device=cuda, generator=g0))
+    gval = _bf(torch.randn((rows, 1), device=cuda, generator=g0))
+    leaves = [t.clone().requires_grad_(True) for t in (h0, w_cat, b_cat, wp2, bp2, wv2, bv2)]
+    h, wc, bc, p2, pb2, v2, vb2 = leaves
+    wp0, wv0, bp0, bv0 = wc[:256], wc[256:], bc[:256], bc[256:]
+    assert K.heads_ok(h0, wp0.detach(), bp0.detach(), wv0.detach(), bv0.detach(), wp2, bp2, wv2, bv2)
+    logits, value = K.HeadsFunction.apply(h, wp0, bp0, wv0, bv0, p2, pb2, v2, vb2)
+    torch.autograd.backward([logits, value], [glog, gval])
+    y = torch._addmm_activation(b_cat, h0, w_cat.t())
+    _bf16_near(y, (h0.double().mm(w_cat.double().t()) + b_cat.double()).clamp_min(0), "y")
+    _bf16_near(logits, y[:, :256].double().mm(wp2.double().t()) + bp2.double(), "logits")
+    _bf16_near(value, y[:, 256:].double().mm(wv2.double().t()) + bv2.double(), "value")
+    dyp = glog.mm(wp2)
+    dyv = _bf(gval.float() * wv2.float())
+    g = torch.where(y > 0, torch.cat([dyp, dyv], 1), torch.zeros_like(y))
+    _bf16_near(h.grad, g.double().mm(w_cat.double()), "dh")
+    _bf16_near(wc.grad, g.double().t().mm(h0.double()), "dW first layers")
+    _bf16_near(bc.grad, g.double().sum(0), "db first layers")
+    _bf16_near(p2.grad, glog.double().t().mm(y[:, :256].double()), "dW policy")
+    _bf16_near(pb2.grad, glog.double().sum(0), "db policy")
+    _bf16_near(v2.grad, gval.double().t().mm(y[:, 256:].double()), "dW value")
+    _bf16_near(vb2.grad, gval.double().sum(0), "db value")
+
+
+def test_network_heads_fused_equals_separate(cuda, monkeypatch):
+    """bf16 raw() forward + backward with the heads as one HeadsFunction == the heads layer by layer: logits
+    and values within a bf16 rounding, every parameter gradient within 1% (relative norm); the Linear
+    shadows lie in one buffer with the heads' first layers adjacent."""
+    import models.network as N
+
+    torch.manual_seed(0)
+    net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    net.train()
+    x = (torch.rand((512, 4, 8, 8), device=cuda) < 0.4).float().contiguous(memory_format=torch.channels_last)
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(N, "HEADS_FUSED", fused)
+        net.load_state_dict(state0)
+        net.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            if fused:
+                h, sh = net._trunk(x)
+                wp0, wv0 = sh[net.policy_head[0]][0], sh[net.value_head[0]][0]
+                assert wv0.data_ptr() == wp0.data_ptr() + 2 * wp0.numel()
+            lo, va = net.raw(x)
+        (lo.float().square().mean() + va.float().sum()).backward()
+        res[fused] = (lo.detach().float(), va.detach().float(), {n: p.grad.clone() for n, p in net.named_parameters()})
+    assert torch.allclose(res[True][0], res[False][0], rtol=2.0 ** -7, atol=1e-3)
+    assert torch.allclose(res[True][1], res[False][1], rtol=2.0 ** -7, atol=1e-3)
+    conv_bias = {n + ".bias" for n, m in net.named_modules() if isinstance(m, torch.nn.Conv2d)}
+    for n, gr in res[True][2].items():
+        if n in conv_bias:
+            continue  # a bias before training-mode BatchNorm: its gradient is 0 up to rounding noise
         ref = res[False][2][n]
         rel = float((gr - ref).norm() / ref.norm().clamp_min(1e-30))
         assert rel < 1e-2, (n, rel)
