@@ -311,6 +311,48 @@ __device__ __forceinline__ bool channel_sums(const double* __restrict__ part, in
   return lane == 0;
 }
 
+// BB_BN_FIN_CPB: channels per finalisation block -- 4: one wave per channel (round 4), 1: the whole block
+// sums one channel (4x the workgroups on the partials' strided rows; each lane a fixed sequence of rows, the
+// lanes' sums by the xor tree, the waves' in order: deterministic).
+#ifndef BB_BN_FIN_CPB
+#define BB_BN_FIN_CPB 1
+#endif
+constexpr int kFinCpb = BB_BN_FIN_CPB;
+static_assert(kFinCpb == 1 || kFinCpb == 4, "BB_BN_FIN_CPB: 1 or 4");
+
+__device__ __forceinline__ bool channel_sums_block(const double* __restrict__ part, int nb, int C, int& c,
+                                                   double a[kQ]) {
+  __shared__ double red[kQ][kBnThreads / 64];
+  c = blockIdx.x;
+  a[0] = a[1] = a[2] = 0.0;
+  int blk = threadIdx.x;
+  for (; blk + kBnThreads < nb; blk += 2 * kBnThreads) {  // two rows' loads in flight
+    double v[2][kQ];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < kQ; ++m) v[j][m] = part[((int64_t)(blk + kBnThreads * j) * C + c) * kQ + m];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < kQ; ++m) a[m] += v[j][m];
+  }
+  if (blk < nb)
+    for (int m = 0; m < kQ; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
+  for (int m = 0; m < kQ; ++m) a[m] = wave_sum(a[m]);
+  if ((threadIdx.x & 63) == 0)
+    for (int m = 0; m < kQ; ++m) red[m][threadIdx.x >> 6] = a[m];
+  __syncthreads();
+  if (threadIdx.x != 0) return false;
+  for (int m = 0; m < kQ; ++m) a[m] = ((red[m][0] + red[m][1]) + red[m][2]) + red[m][3];
+  return true;
+}
+
+__device__ __forceinline__ bool fin_sums(const double* __restrict__ part, int nb, int C, int& c, double a[kQ]) {
+  if (kFinCpb == 1) return channel_sums_block(part, nb, C, c, a);
+  return channel_sums(part, nb, C, c, a);
+}
+
 // Forward finalisation: mean, inverse std of the biased variance (the
 // normalisation), running statistics with the unbiased variance
 // (nn.BatchNorm2d, momentum = exponential_average_factor), num_batches_tracked
@@ -325,7 +367,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_fwd(const double* __re
                                                               float* __restrict__ coef) {
   int c;
   double a[kQ];
-  if (!channel_sums(part, nb, C, c, a)) return;
+  if (!fin_sums(part, nb, C, c, a)) return;
   const double m = a[0] / M;  // mean of x (the bias-free input)
   double var = a[1] / M - m * m;
   if (var < 0.0) var = 0.0;
@@ -343,7 +385,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_fwd(const double* __re
 // Backward finalisation: dweight = sum(g * xhat), dbias = sum(g), the
 // convolution bias gradient sum(dx) (dx = sc * (g - mg - xhat * mgx) summed in
 // fp64), coefficients.
-// With a WgradReduceJob (bb_bn_backward_red): blocks from (C + 3) / 4 on add a preceding board convolution's
+// With a WgradReduceJob (bb_bn_backward_red): blocks from the finalisation's on add a preceding board convolution's
 // weight-gradient partials instead -- two independent small passes in one launch.
 __global__ void __launch_bounds__(kBnThreads) bn_finalize_bwd(const double* __restrict__ part, int nb, int C, double M,
                                                               const float* __restrict__ pre_bias,
@@ -352,14 +394,14 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_bwd(const double* __re
                                                               const float* __restrict__ invstd, float* __restrict__ dw,
                                                               float* __restrict__ db, float* __restrict__ dpb,
                                                               float* __restrict__ coef, WgradReduceJob job) {
-  const int fin_blocks = (C + 3) / 4;
+  const int fin_blocks = (C + kFinCpb - 1) / kFinCpb;
   if ((int)blockIdx.x >= fin_blocks) {
     wgrad_reduce_at(job, ((int)blockIdx.x - fin_blocks) * kBnThreads + threadIdx.x);
     return;
   }
   int c;
   double a[kQ];
-  if (!channel_sums(part, nb, C, c, a)) return;
+  if (!fin_sums(part, nb, C, c, a)) return;
   const float invM = (float)(1.0 / M);
   const double sg = a[0], sgx = a[1], sx = a[2];
   const float is = invstd[c], sc = is * w[c];
@@ -537,7 +579,7 @@ hipError_t bn_forward_t(const void* x, const void* res, int nhwc, int N, int C, 
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
   launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, k.part, s);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + 3) / 4), dim3(kBnThreads), 0, s, k.part, p.nb, C, (double)N * HW, eps,
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + kFinCpb - 1) / kFinCpb), dim3(kBnThreads), 0, s, k.part, p.nb, C, (double)N * HW, eps,
                      pb, w, b, save_mean, save_invstd, rmean, rvar, momentum, nbt, k.coef);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
@@ -566,7 +608,7 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
     jb = *job;
     red_blocks = (9 * jb.cout * jb.cin + kBnThreads - 1) / kBnThreads;
   }
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + 3) / 4 + red_blocks), dim3(kBnThreads), 0, s, k.part, p.nb, C,
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kFinCpb - 1) / kFinCpb + red_blocks), dim3(kBnThreads), 0, s, k.part, p.nb, C,
                      (double)N * HW, pb, w, b, mean, invstd, dw, db, dpb, k.coef, jb);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)

@@ -23,6 +23,8 @@ VARIANTS = {
     # the round-3 compile-time variants measured slower were removed (tools/patches/r03_compile_variants.diff
     # restores them), so their A/B arms cannot be rebuilt from this tree.
     "main": [],
+    # BatchNorm finalisation: one wave per channel (round 4) instead of one workgroup
+    "fin4": ["-DBB_BN_FIN_CPB=4"],
     # round 5: search waves' pass schedule -- 0: gen_hands_multi's packed passes (round 4); quota per attempt
     # in a round's first pass (shipped 4) and later passes (shipped 64)
     "mq0": ["-DBB_SEARCH_QUOTA=0"],
