@@ -97,25 +97,61 @@ __device__ double block_sum(double x, double* red) {
   return s;
 }
 
+// BB_ADAM_NORM_CPB chunks per workgroup, their loads all in flight before the adds; every chunk's sum is its
+// own partial, added in the same order for any setting (bit-identical partials).  4: 15.2 us vs 11.0 us for
+// one chunk per workgroup (fewer workgroups in flight; tools/variants.py an4).
+#ifndef BB_ADAM_NORM_CPB
+#define BB_ADAM_NORM_CPB 1
+#endif
+constexpr int kNormCpb = BB_ADAM_NORM_CPB;
+
 __global__ void __launch_bounds__(kOptThreads) adam_norm_kernel(const AdamTable tab, double* __restrict__ ws) {
-  __shared__ double red[kOptThreads / 64];
-  const int chunk = blockIdx.x;
-  const int t = find_tensor(tab, chunk);
-  const int64_t base = int64_t(chunk - tab.chunk0[t]) * kOptChunk;
-  const int64_t n = tab.n[t];
-  const float* g = tab.g[t];
-  float acc = 0.f;
-  const int64_t i0 = base + threadIdx.x * 4;
-  if (((reinterpret_cast<uintptr_t>(g) & 15) == 0) && base + kOptChunk <= n) {
-    for (int k = 0; k < kOptChunk; k += kOptThreads * 4) {
-      const float4 q = *reinterpret_cast<const float4*>(g + i0 + k);
-      acc += q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+  __shared__ double red[kNormCpb][kOptThreads / 64];
+  constexpr int L = kOptChunk / (kOptThreads * 4);  // float4 loads per thread per chunk
+  const int nchunks = tab.chunk0[tab.count];
+  float acc[kNormCpb];
+  float4 q[kNormCpb][L];
+  bool fast[kNormCpb];
+#pragma unroll
+  for (int j = 0; j < kNormCpb; ++j) {
+    acc[j] = 0.f;
+    const int chunk = blockIdx.x * kNormCpb + j;
+    fast[j] = false;
+    if (chunk >= nchunks) continue;
+    const int t = find_tensor(tab, chunk);
+    const int64_t base = int64_t(chunk - tab.chunk0[t]) * kOptChunk;
+    const float* g = tab.g[t];
+    fast[j] = ((reinterpret_cast<uintptr_t>(g) & 15) == 0) && base + kOptChunk <= tab.n[t];
+    if (fast[j]) {
+#pragma unroll
+      for (int k = 0; k < L; ++k)
+        q[j][k] = *reinterpret_cast<const float4*>(g + base + threadIdx.x * 4 + k * kOptThreads * 4);
+    } else {
+      for (int64_t i = base + threadIdx.x; i < tab.n[t] && i < base + kOptChunk; i += kOptThreads)
+        acc[j] += g[i] * g[i];
     }
-  } else {
-    for (int64_t i = base + threadIdx.x; i < n && i < base + kOptChunk; i += kOptThreads) acc += g[i] * g[i];
   }
-  const double s = block_sum(double(acc), red);
-  if (threadIdx.x == 0) ws[kHdr + chunk] = s;
+#pragma unroll
+  for (int j = 0; j < kNormCpb; ++j)
+    if (fast[j])
+#pragma unroll
+      for (int k = 0; k < L; ++k) acc[j] += q[j][k].x * q[j][k].x + q[j][k].y * q[j][k].y + q[j][k].z * q[j][k].z +
+                                           q[j][k].w * q[j][k].w;
+  // block_sum's fixed-order tree, per chunk
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < kNormCpb; ++j) {
+    double x = double(acc[j]);
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    if (lane == 0) red[j][w] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < kNormCpb) {
+    const int chunk = blockIdx.x * kNormCpb + threadIdx.x;
+    double s = 0.0;
+    for (int i = 0; i < kOptThreads / 64; ++i) s += red[threadIdx.x][i];
+    if (chunk < nchunks) ws[kHdr + chunk] = s;
+  }
 }
 
 __global__ void __launch_bounds__(kOptThreads) adam_finalize_kernel(const AdamTable tab, double* __restrict__ ws,
@@ -124,7 +160,15 @@ __global__ void __launch_bounds__(kOptThreads) adam_finalize_kernel(const AdamTa
   __shared__ double red[kOptThreads / 64];
   const int nchunks = tab.chunk0[tab.count];
   double s = 0.0;
-  for (int i = threadIdx.x; i < nchunks; i += kOptThreads) s += ws[kHdr + i];
+  int i = threadIdx.x;
+  for (; i + 7 * kOptThreads < nchunks; i += 8 * kOptThreads) {  // 8 loads in flight, added in order
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ws[kHdr + i + j * kOptThreads];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+  }
+  for (; i < nchunks; i += kOptThreads) s += ws[kHdr + i];
   s = block_sum(s, red);
   float* hdr = reinterpret_cast<float*>(ws);
   if (threadIdx.x == 0) {
@@ -764,7 +808,7 @@ hipError_t launch_adam_clip(int count, float* const* p, float* const* g, float* 
   AdamTable tab;
   const int chunks = build_adam_table(tab, count, p, g, m, v, step, n);
   if (chunks <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(adam_norm_kernel, dim3(chunks), dim3(kOptThreads), 0, s, tab, ws);
+  hipLaunchKernelGGL(adam_norm_kernel, dim3((chunks + kNormCpb - 1) / kNormCpb), dim3(kOptThreads), 0, s, tab, ws);
   hipLaunchKernelGGL(adam_finalize_kernel, dim3(1), dim3(kOptThreads), 0, s, tab, ws, max_norm, beta1, beta2,
                      norm_out);
   hipLaunchKernelGGL(adam_update_kernel, dim3(chunks), dim3(kOptThreads), 0, s, tab, ws, lr, beta1, beta2, eps);
