@@ -651,7 +651,7 @@ int bn_forward_impl(const void* d_x, const void* d_res, int32_t dtype, int32_t n
                     const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps, int32_t relu,
                     double* d_ws, float* d_save_mean, float* d_save_invstd, float* d_running_mean,
                     float* d_running_var, float momentum, int64_t* d_num_batches_tracked, void* d_y, void* stream,
-                    const char* what) {
+                    const char* what, const double* d_part = nullptr, int32_t nb_part = 0) {
   int rc = bn_check(dtype, nhwc, N, C, HW);
   if (rc != BB_OK) return rc;
   if (!d_x || !d_weight || !d_bias || !d_ws || !d_save_mean || !d_save_invstd || !d_y)
@@ -661,11 +661,23 @@ int bn_forward_impl(const void* d_x, const void* d_res, int32_t dtype, int32_t n
     return fail(nullptr, BB_ERR_ARG, "bb_bn: d_res must be 16-byte aligned");
   hipError_t st = launch_bn_forward(d_x, d_res, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
                                     d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum,
-                                    d_num_batches_tracked, d_y, (hipStream_t)stream);
+                                    d_num_batches_tracked, d_y, (hipStream_t)stream, d_part, nb_part);
   if (st != hipSuccess) return hip_fail(nullptr, st, what);
   return BB_OK;
 }
 }  // namespace
+
+extern "C" int bb_bn_forward_part(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N,
+                                  int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
+                                  const float* d_bias, float eps, int32_t relu, double* d_ws, float* d_save_mean,
+                                  float* d_save_invstd, float* d_running_mean, float* d_running_var, float momentum,
+                                  int64_t* d_num_batches_tracked, void* d_y, const double* d_part, int32_t nb_part,
+                                  void* stream) {
+  if (!d_part || nb_part <= 0) return fail(nullptr, BB_ERR_ARG, "bb_bn_forward_part: no statistics partials");
+  return bn_forward_impl(d_x, d_res, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, eps, relu, d_ws,
+                         d_save_mean, d_save_invstd, d_running_mean, d_running_var, momentum, d_num_batches_tracked,
+                         d_y, stream, "bb_bn_forward_part", d_part, nb_part);
+}
 
 extern "C" int bb_bn_forward(const void* d_x, int32_t dtype, int32_t nhwc, int32_t N, int32_t C, int32_t HW,
                              const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps,
@@ -886,6 +898,24 @@ extern "C" int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, i
     return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward: tensors must be 16-byte aligned");
   hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream);
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward");
+  return BB_OK;
+}
+
+extern "C" int32_t bb_conv3x3_stats_blocks(int32_t N, int32_t cout) {
+  return (cout == 64 || cout == 128) ? conv3x3_stats_blocks(N, cout) : -1;
+}
+
+extern "C" int bb_conv3x3_forward_stats(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout,
+                                        void* d_y, double* d_part, void* stream) {
+  int rc = conv_check(N, cin, cout, "bb_conv3x3_forward_stats");
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_w || !d_y || !d_part) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: NULL argument");
+  if (!al16(d_x) || !al16(d_w) || !al16(d_y))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: tensors must be 16-byte aligned");
+  hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream, nullptr, d_part);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: not available in this (variant) build");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward_stats");
   return BB_OK;
 }
 

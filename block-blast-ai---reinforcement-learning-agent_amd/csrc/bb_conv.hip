@@ -210,11 +210,17 @@ __device__ __forceinline__ uint32_t add2_bf16(uint32_t a, uint32_t b) {  // two 
 // radd (NULL = none, shipped LDS-staged store path only): y = bf16(conv) + radd, rounded again -- the
 // data gradient of a ResidualBlock's first convolution plus the identity path's gradient, as autograd's
 // separate add kernel computed it
+// stats (NULL = none, same path, radd NULL): the following BatchNorm's batch statistics from the store pass --
+// per channel, the sum and the sum of squares of the stored bf16 outputs over the workgroup's pixels (f32 per
+// thread over its rows, the lanes of a channel by a fixed xor tree, the waves added in order in f64) ->
+// stats[(blockIdx.x * COUT + c) * 3 + {0, 1, 2 (= 0)}]: bn_reduce_nhwc's partial layout, so the BatchNorm
+// forward finalises from them without its own pass over the output (bb_bn_forward_part)
 template <int CIN, int COUT>
 __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ y, int nb,
-                                                               const uint16_t* __restrict__ radd) {
+                                                               const uint16_t* __restrict__ radd,
+                                                               double* __restrict__ stats) {
   constexpr int RB = CIN * 2;                 // bytes per pixel row
   constexpr int NCH = CIN / 8;                // 16-byte chunks per pixel row
   constexpr int FB = fwd_boards<COUT>();
@@ -408,6 +414,10 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
     }
   }
   __syncthreads();
+  static_assert(kFwdThreads % OCH == 0, "a thread's output chunk column must stay fixed");
+  float ss[8], sq[8];  // stats: the 8 channels of chunk column tid % OCH
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss[j] = sq[j] = 0.f;
   for (int e = tid; e < ROWS * OCH; e += kFwdThreads) {
     const int px = e / OCH, c = e % OCH;
     if (b0 + (px >> 6) >= nb) continue;
@@ -418,7 +428,44 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
       const uint4 a = *reinterpret_cast<const uint4*>(radd + o);
       v = make_uint4(add2_bf16(v.x, a.x), add2_bf16(v.y, a.y), add2_bf16(v.z, a.z), add2_bf16(v.w, a.w));
     }
+    if (stats) {
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = __uint_as_float(vv[k] << 16), hi = __uint_as_float(vv[k] & 0xFFFF0000u);
+        ss[2 * k] += lo;
+        sq[2 * k] += lo * lo;
+        ss[2 * k + 1] += hi;
+        sq[2 * k + 1] += hi * hi;
+      }
+    }
     *reinterpret_cast<uint4*>(y + o) = v;
+  }
+  if (stats) {  // uniform: every thread reaches the barrier
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int m = OCH; m < 64; m <<= 1) {
+        ss[j] += __shfl_xor(ss[j], m, 64);
+        sq[j] += __shfl_xor(sq[j], m, 64);
+      }
+    float* red = reinterpret_cast<float*>(sm + ROWS * COUT * 2);  // past the output tile: [wave][2][COUT]
+    static_assert(ROWS * COUT * 2 + NW * 2 * COUT * 4 <= XBYTES + kFwdRing * WBYTES, "stats scratch");
+    if (lane < OCH)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wid * 2 + 0) * COUT + lane * 8 + j] = ss[j];
+        red[(wid * 2 + 1) * COUT + lane * 8 + j] = sq[j];
+      }
+    __syncthreads();
+    for (int t = tid; t < COUT * 3; t += kFwdThreads) {
+      const int c = t / 3, m = t % 3;
+      double a = 0.0;
+      if (m < 2)
+#pragma unroll
+        for (int wv = 0; wv < NW; ++wv) a += (double)red[(wv * 2 + m) * COUT + c];
+      stats[(size_t)blockIdx.x * COUT * 3 + t] = a;
+    }
   }
 #else
 #pragma unroll
@@ -789,11 +836,13 @@ int wgrad_bpc(int nb, int nchunk) {
 }
 
 template <int CIN, int COUT>
-hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr) {
-  if (nb <= 0) return hipErrorInvalidValue;
-  if (radd && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS)) return hipErrorInvalidValue;  // variant builds: no fused add
+hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr,
+                 double* stats = nullptr) {
+  if (nb <= 0 || (radd && stats)) return hipErrorInvalidValue;
+  // variant builds: no fused add / statistics
+  if ((radd || stats) && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS)) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>()), dim3(kFwdThreads), 0, s,
-                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd);
+                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd, stats);
   return hipGetLastError();
 }
 
@@ -1111,11 +1160,17 @@ hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int
 }
 
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
-                                  const void* radd) {
-  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s, radd);
-  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd);
-  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd);
-  return fwd_t<128, 128>(x, w, nb, y, s, radd);
+                                  const void* radd, double* stats) {
+  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s, radd, stats);
+  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd, stats);
+  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd, stats);
+  return fwd_t<128, 128>(x, w, nb, y, s, radd, stats);
+}
+
+int conv3x3_stats_blocks(int nb, int cout) {
+  if (nb <= 0) return -1;
+  const int fb = cout == 128 ? fwd_boards<128>() : fwd_boards<64>();
+  return (nb + fb - 1) / fb;
 }
 
 int conv3x3_wgrad_chunks_used(int nb, int cin, int cout) { return wgrad_used(nb, cin, cout); }

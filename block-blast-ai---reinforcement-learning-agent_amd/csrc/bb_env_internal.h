@@ -106,7 +106,7 @@ int64_t bn_workspace_bytes(int dtype, int nhwc, int N, int C, int HW);
 hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc, int N, int C, int HW,
                              const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
                              float* save_mean, float* save_invstd, float* rmean, float* rvar, float momentum,
-                             int64_t* nbt, void* y, hipStream_t s);
+                             int64_t* nbt, void* y, hipStream_t s, const double* ext_part = nullptr, int ext_nb = 0);
 // a board convolution's weight-gradient partial-sum reduction (csrc/bb_conv.hip conv_wgrad_reduce's arguments),
 // run inside a BatchNorm backward finalisation's launch by bb_bn_backward_red
 struct WgradReduceJob {  // conv_wgrad_reduce's arguments
@@ -125,7 +125,8 @@ hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* 
 hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
                                      const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s);
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
-                                  const void* radd = nullptr);
+                                  const void* radd = nullptr, double* stats = nullptr);
+int conv3x3_stats_blocks(int nb, int cout);
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);
 // the weight gradient in two parts: the partial-sum kernel, and the fixed-order sum of its `used` chunks (which

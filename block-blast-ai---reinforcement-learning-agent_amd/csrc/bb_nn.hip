@@ -320,6 +320,8 @@ __device__ __forceinline__ bool channel_sums(const double* __restrict__ part, in
 constexpr int kFinCpb = BB_BN_FIN_CPB;
 static_assert(kFinCpb == 1 || kFinCpb == 4, "BB_BN_FIN_CPB: 1 or 4");
 
+// NQR: the quantities read (the forward's third is 0 and skipped)
+template <int NQR>
 __device__ __forceinline__ bool channel_sums_block(const double* __restrict__ part, int nb, int C, int& c,
                                                    double a[kQ]) {
   __shared__ double red[kQ][kBnThreads / 64];
@@ -327,18 +329,19 @@ __device__ __forceinline__ bool channel_sums_block(const double* __restrict__ pa
   a[0] = a[1] = a[2] = 0.0;
   int blk = threadIdx.x;
   for (; blk + kBnThreads < nb; blk += 2 * kBnThreads) {  // two rows' loads in flight
-    double v[2][kQ];
+    double v[2][NQR];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int m = 0; m < kQ; ++m) v[j][m] = part[((int64_t)(blk + kBnThreads * j) * C + c) * kQ + m];
+      for (int m = 0; m < NQR; ++m) v[j][m] = part[((int64_t)(blk + kBnThreads * j) * C + c) * kQ + m];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int m = 0; m < kQ; ++m) a[m] += v[j][m];
+      for (int m = 0; m < NQR; ++m) a[m] += v[j][m];
   }
   if (blk < nb)
-    for (int m = 0; m < kQ; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
+#pragma unroll
+    for (int m = 0; m < NQR; ++m) a[m] += part[((int64_t)blk * C + c) * kQ + m];
   for (int m = 0; m < kQ; ++m) a[m] = wave_sum(a[m]);
   if ((threadIdx.x & 63) == 0)
     for (int m = 0; m < kQ; ++m) red[m][threadIdx.x >> 6] = a[m];
@@ -348,8 +351,9 @@ __device__ __forceinline__ bool channel_sums_block(const double* __restrict__ pa
   return true;
 }
 
+template <int NQR = kQ>
 __device__ __forceinline__ bool fin_sums(const double* __restrict__ part, int nb, int C, int& c, double a[kQ]) {
-  if (kFinCpb == 1) return channel_sums_block(part, nb, C, c, a);
+  if (kFinCpb == 1) return channel_sums_block<NQR>(part, nb, C, c, a);
   return channel_sums(part, nb, C, c, a);
 }
 
@@ -367,7 +371,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_fwd(const double* __re
                                                               float* __restrict__ coef) {
   int c;
   double a[kQ];
-  if (!fin_sums(part, nb, C, c, a)) return;
+  if (!fin_sums<2>(part, nb, C, c, a)) return;
   const double m = a[0] / M;  // mean of x (the bias-free input)
   double var = a[1] / M - m * m;
   if (var < 0.0) var = 0.0;
@@ -575,11 +579,15 @@ Ws split_ws(double* ws, int C) {
 template <typename T>
 hipError_t bn_forward_t(const void* x, const void* res, int nhwc, int N, int C, int HW, const float* pb, const float* w,
                         const float* b, float eps, int relu, double* ws, float* save_mean, float* save_invstd,
-                        float* rmean, float* rvar, float momentum, int64_t* nbt, void* y, hipStream_t s) {
+                        float* rmean, float* rvar, float momentum, int64_t* nbt, void* y, hipStream_t s,
+                        const double* ext_part, int ext_nb) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
-  launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, k.part, s);
-  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + kFinCpb - 1) / kFinCpb), dim3(kBnThreads), 0, s, k.part, p.nb, C, (double)N * HW, eps,
+  // ext_part: the block partials a preceding board convolution's store pass produced (conv_fwd_kernel stats)
+  const double* part = ext_part ? ext_part : k.part;
+  const int nbp = ext_part ? ext_nb : p.nb;
+  if (!ext_part) launch_reduce<T, false>(p, nhwc, x, nullptr, N, C, HW, pb, w, b, nullptr, nullptr, 0, k.part, s);
+  hipLaunchKernelGGL(bn_finalize_fwd, dim3((C + kFinCpb - 1) / kFinCpb), dim3(kBnThreads), 0, s, part, nbp, C, (double)N * HW, eps,
                      pb, w, b, save_mean, save_invstd, rmean, rvar, momentum, nbt, k.coef);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
@@ -630,12 +638,12 @@ int64_t bn_workspace_bytes(int dtype, int nhwc, int N, int C, int HW) {
 hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc, int N, int C, int HW,
                              const float* pb, const float* w, const float* b, float eps, int relu, double* ws,
                              float* save_mean, float* save_invstd, float* rmean, float* rvar, float momentum,
-                             int64_t* nbt, void* y, hipStream_t s) {
+                             int64_t* nbt, void* y, hipStream_t s, const double* ext_part, int ext_nb) {
   if (dtype == 1)
     return bn_forward_t<__hip_bfloat16>(x, res, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean,
-                                        rvar, momentum, nbt, y, s);
+                                        rvar, momentum, nbt, y, s, ext_part, ext_nb);
   return bn_forward_t<float>(x, res, nhwc, N, C, HW, pb, w, b, eps, relu, ws, save_mean, save_invstd, rmean, rvar, momentum,
-                             nbt, y, s);
+                             nbt, y, s, ext_part, ext_nb);
 }
 
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,

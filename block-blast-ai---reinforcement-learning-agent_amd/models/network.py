@@ -41,15 +41,16 @@ class BatchNorm2d(nn.BatchNorm2d):
 
         return bn_fusable(x)
 
-    def forward(self, x: torch.Tensor, pre_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, pre_bias: Optional[torch.Tensor] = None, stats=None) -> torch.Tensor:
         """BatchNorm2d(x + pre_bias) [-> ReLU]; ``pre_bias`` is a preceding
-        convolution's bias that was left out of the convolution."""
+        convolution's bias that was left out of the convolution; ``stats`` its
+        runtime.kernels.StatsSlot (the batch statistics from its store pass)."""
         if self.fusable(x):
             from runtime.kernels import BatchNormReLUFunction
 
             return BatchNormReLUFunction.apply(x, pre_bias, self.weight, self.bias, self.running_mean,
                                                self.running_var, self.momentum, self.eps, self.fuse_relu,
-                                               self.num_batches_tracked)  # += 1 in the finalize kernel
+                                               self.num_batches_tracked, stats)  # += 1 in the finalize kernel
         if pre_bias is not None:
             x = x + pre_bias.view(1, -1, 1, 1).to(x.dtype)
         y = super().forward(x)
@@ -107,7 +108,7 @@ def _hip_conv_on(x: torch.Tensor) -> bool:
         and torch.get_autocast_dtype("cuda") == torch.bfloat16
 
 
-def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> torch.Tensor:
+def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None, stats=None) -> torch.Tensor:
     """conv(x) without its bias.  Under bf16 autocast on the GPU the 3x3
     layers with 64 or 128 channels in and out run on the HIP kernels
     (runtime.kernels.Conv3x3Function): bf16 NHWC, f32 accumulation, as
@@ -120,7 +121,7 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> 
         if conv3x3_fusable(x, conv):
             if prep is not None:
                 prep.run()
-            return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox)
+            return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox, stats)
         if conv_in_fusable(x, conv):  # the 4 -> 64 input layer: f32 boards in, bf16 NHWC out (+ the images)
             return ConvInFunction.apply(x, conv.weight, prep)
     elif _f32_conv_on(x, conv):
@@ -130,15 +131,25 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None) -> 
     return conv._conv_forward(x, conv.weight, None)
 
 
+def _stats_slot(x: torch.Tensor):
+    """A StatsSlot for a HIP board convolution feeding one of our BatchNorms (None off that path)."""
+    if not _hip_conv_on(x):
+        return None
+    from runtime.kernels import StatsSlot
+
+    return StatsSlot()
+
+
 def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None, mailbox=None) -> torch.Tensor:
     """bn(conv(x)).  When the BatchNorm runs on the HIP kernels the
     convolution's bias is added inside them (one add on load instead of a
     separate pass, and its gradient comes out of the BatchNorm backward instead
     of a reduction over dy)."""
     if isinstance(bn, BatchNorm2d) and conv.bias is not None and bn.training and x.is_cuda and bn.use_fused:
-        z = conv_nobias(conv, x, images, mailbox)
+        slot = _stats_slot(x)
+        z = conv_nobias(conv, x, images, mailbox, slot)
         if bn.fusable(z):
-            return bn(z, pre_bias=conv.bias)
+            return bn(z, pre_bias=conv.bias, stats=slot)
         return bn(z + conv.bias.view(1, -1, 1, 1).to(z.dtype))
     return bn(conv(x))
 
@@ -185,16 +196,17 @@ class ResidualBlock(nn.Module):
                 mailbox = GradMailbox()
         y = conv_bn(self.conv1, self.bn1, x, images, mailbox)
         if fused:
-            z = conv_nobias(conv2, y, images)
+            slot = _stats_slot(y)
+            z = conv_nobias(conv2, y, images, None, slot)
             from runtime.kernels import BatchNormAddReLUFunction, _bn_layout
 
             if bn2.fusable(z) and x.dtype == z.dtype and x.shape == z.shape and _bn_layout(x) == _bn_layout(z):
                 # bn2 -> + identity -> relu in the BatchNorm apply pass
                 return BatchNormAddReLUFunction.apply(z, conv2.bias, x, bn2.weight, bn2.bias, bn2.running_mean,
                                                       bn2.running_var, bn2.momentum, bn2.eps,
-                                                      bn2.num_batches_tracked, mailbox)
+                                                      bn2.num_batches_tracked, mailbox, slot)
             # (an unused mailbox stays empty: conv1's data gradient is then the plain one, and autograd adds)
-            return F.relu(bn2(z, pre_bias=conv2.bias) + x)
+            return F.relu(bn2(z, pre_bias=conv2.bias, stats=slot) + x)
         y = conv_bn(conv2, bn2, y, images)
         return F.relu(y + x)
 

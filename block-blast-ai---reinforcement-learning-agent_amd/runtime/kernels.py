@@ -154,6 +154,28 @@ def bn_fusable(x: torch.Tensor) -> bool:
     return (x.shape[2] * x.shape[3] * x.element_size()) % 16 == 0
 
 
+# BatchNorm batch statistics from the producing convolution's store pass (bb_conv3x3_forward_stats ->
+# bb_bn_forward_part): no reduction pass over the convolution's output (0: bb_bn_forward's own pass, for A/B)
+CONV_STATS = os.environ.get("BB_CONV_STATS", "1") != "0"
+
+
+class StatsSlot:
+    """Carries bb_conv3x3_forward_stats' partials from a board convolution to the BatchNorm reading its output."""
+
+    __slots__ = ("part", "nb", "ptr")
+
+    def __init__(self):
+        self.part, self.nb, self.ptr = None, 0, 0
+
+
+def _stats_for(slot, x: torch.Tensor):
+    """(partials, blocks) when ``slot`` holds the statistics of exactly x (bf16 NHWC), else None."""
+    if slot is None or slot.part is None or slot.ptr != x.data_ptr() or x.dtype != torch.bfloat16 \
+            or not _bn_layout(x):
+        return None
+    return slot.part, slot.nb
+
+
 def _bn_workspace(x: torch.Tensor, nhwc: int) -> torch.Tensor:
     n, c, h, w = x.shape
     nbytes = L.load().bb_bn_workspace_bytes(_BN_DTYPES[x.dtype], nhwc, n, c, h * w)
@@ -187,7 +209,7 @@ class BatchNormReLUFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, pre_bias, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool,
-                num_batches_tracked=None):
+                num_batches_tracked=None, stats=None):
         nhwc = _bn_layout(x)
         x = x.contiguous(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         n, c, h, w = x.shape
@@ -196,11 +218,15 @@ class BatchNormReLUFunction(torch.autograd.Function):
         ws = _bn_workspace(x, nhwc)
         mean = torch.empty(c, dtype=torch.float32, device=dev)
         invstd = torch.empty(c, dtype=torch.float32, device=dev)
-        L.check(L.load().bb_bn_forward(_p(x), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight),
-                                       _p(bias), float(eps), int(relu), _p(ws), _p(mean), _p(invstd),
-                                       _p(running_mean), _p(running_var), float(momentum),
-                                       _p(num_batches_tracked), _p(y), _s(dev)),
-                "bb_bn_forward")
+        args = (_p(x), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight), _p(bias), float(eps),
+                int(relu), _p(ws), _p(mean), _p(invstd), _p(running_mean), _p(running_var), float(momentum),
+                _p(num_batches_tracked), _p(y))
+        st = _stats_for(stats, x)
+        if st is None:
+            L.check(L.load().bb_bn_forward(*args, _s(dev)), "bb_bn_forward")
+        else:  # the statistics came out of the convolution's store pass
+            L.check(L.load().bb_bn_forward_part(args[0], None, *args[1:], _p(st[0]), st[1], _s(dev)),
+                    "bb_bn_forward_part")
         ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd)
         ctx.relu = bool(relu)
         ctx.nhwc = nhwc
@@ -220,7 +246,7 @@ class BatchNormReLUFunction(torch.autograd.Function):
         ws = _bn_workspace(x, ctx.nhwc)
         _bn_backward_call(x, dy, ctx.nhwc, pre_bias, weight, bias, mean, invstd, int(ctx.relu), ws, dx, dw, db, dpb,
                           dev)
-        return dx, dpb, dw, db, None, None, None, None, None, None
+        return dx, dpb, dw, db, None, None, None, None, None, None, None
 
 
 # ResidualBlock tail backward on bb_bn_backward_res: the ReLU mask applied in the BatchNorm reduction, which
@@ -241,7 +267,7 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, pre_bias, res, weight, bias, running_mean, running_var, momentum: float, eps: float,
-                num_batches_tracked=None, grad_mailbox=None):
+                num_batches_tracked=None, grad_mailbox=None, stats=None):
         ctx.mailbox = grad_mailbox
         nhwc = _bn_layout(x)
         fmt = torch.channels_last if nhwc else torch.contiguous_format
@@ -253,11 +279,14 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
         ws = _bn_workspace(x, nhwc)
         mean = torch.empty(c, dtype=torch.float32, device=dev)
         invstd = torch.empty(c, dtype=torch.float32, device=dev)
-        L.check(L.load().bb_bn_forward_res(_p(x), _p(res), _BN_DTYPES[x.dtype], nhwc, n, c, h * w,
-                                           _p(pre_bias), _p(weight), _p(bias), float(eps), 1, _p(ws), _p(mean),
-                                           _p(invstd), _p(running_mean), _p(running_var), float(momentum),
-                                           _p(num_batches_tracked), _p(y), _s(dev)),
-                "bb_bn_forward_res")
+        args = (_p(x), _p(res), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight), _p(bias),
+                float(eps), 1, _p(ws), _p(mean), _p(invstd), _p(running_mean), _p(running_var), float(momentum),
+                _p(num_batches_tracked), _p(y))
+        st = _stats_for(stats, x)
+        if st is None:
+            L.check(L.load().bb_bn_forward_res(*args, _s(dev)), "bb_bn_forward_res")
+        else:  # the statistics came out of the convolution's store pass
+            L.check(L.load().bb_bn_forward_part(*args, _p(st[0]), st[1], _s(dev)), "bb_bn_forward_part")
         ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd, y)
         ctx.nhwc = nhwc
         return y
@@ -291,7 +320,7 @@ class BatchNormAddReLUFunction(torch.autograd.Function):
         if ctx.mailbox is not None and ctx.needs_input_grad[2]:
             ctx.mailbox.put(g)  # the block's first convolution adds it to its data gradient
             gres = None
-        return dx, dpb, gres, dw, db, None, None, None, None, None, None
+        return dx, dpb, gres, dw, db, None, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -497,7 +526,7 @@ class Conv3x3Function(torch.autograd.Function):
     kernel over dy with the tap-reversed, transposed weight image)."""
 
     @staticmethod
-    def forward(ctx, x, weight, images=None, grad_mailbox=None):
+    def forward(ctx, x, weight, images=None, grad_mailbox=None, stats=None):
         _need_cuda(x, weight)
         ctx.mailbox = grad_mailbox
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -513,7 +542,14 @@ class Conv3x3Function(torch.autograd.Function):
             wd = torch.empty(9 * cout * cin, dtype=torch.bfloat16, device=dev)
             L.check(lib.bb_conv3x3_prep(_p(weight), cin, cout, wl, _p(wf), _p(wd), _s(dev)), "bb_conv3x3_prep")
         y = torch.empty((n, cout, 8, 8), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
-        L.check(lib.bb_conv3x3_forward(_p(x), _p(wf), n, cin, cout, _p(y), _s(dev)), "bb_conv3x3_forward")
+        if stats is not None and CONV_STATS:  # + the following BatchNorm's statistics partials (StatsSlot)
+            nbp = lib.bb_conv3x3_stats_blocks(n, cout)
+            part = torch.empty(nbp * cout * 3, dtype=torch.float64, device=dev)
+            L.check(lib.bb_conv3x3_forward_stats(_p(x), _p(wf), n, cin, cout, _p(y), _p(part), _s(dev)),
+                    "bb_conv3x3_forward_stats")
+            stats.part, stats.nb, stats.ptr = part, nbp, y.data_ptr()
+        else:
+            L.check(lib.bb_conv3x3_forward(_p(x), _p(wf), n, cin, cout, _p(y), _s(dev)), "bb_conv3x3_forward")
         ctx.save_for_backward(x, wd, weight)
         return y
 
@@ -562,7 +598,7 @@ class Conv3x3Function(torch.autograd.Function):
                 st[2].append((weight, dw.data_ptr()))
             elif not _wgrad_deferred(weight, dev, (x, dy), wgrad):
                 dw = wgrad()
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 _CONV32_PAIRS = ((128, 128), (64, 128))  # forward layers; the 64 -> 128 layer's data gradient runs (128, 64)

@@ -42,7 +42,8 @@ extern "C" {
                                  bb_conv_in_forward / _wgrad; bb_bn_backward_res; bb_ppo_loss_fused and the
                                  loss forward's d_cnt (one launch, the statistics finalised in it);
                                  bb_conv3x3_wgrad_partial / _reduce / _chunks, bb_bn_backward_red,
-                                 bb_conv_in_forward_prep, bb_linear_bgrad2 */
+                                 bb_conv_in_forward_prep, bb_linear_bgrad2, bb_conv3x3_forward_stats,
+                                 bb_conv3x3_stats_blocks, bb_bn_forward_part */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -327,6 +328,14 @@ int bb_bn_forward_res(const void* d_x, const void* d_res, int32_t dtype, int32_t
                       const float* d_bias, float eps, int32_t relu, double* d_ws, float* d_save_mean,
                       float* d_save_invstd, float* d_running_mean, float* d_running_var, float momentum,
                       int64_t* d_num_batches_tracked, void* d_y, void* stream);
+/* bb_bn_forward (d_res NULL) or bb_bn_forward_res from statistics partials a board convolution's forward
+ * already produced (bb_conv3x3_forward_stats: d_part [nb_part][C][3] doubles, nb_part =
+ * bb_conv3x3_stats_blocks(N, C)) instead of its own reduction pass over x: two launches (ABI 8). */
+int bb_bn_forward_part(const void* d_x, const void* d_res, int32_t dtype, int32_t nhwc, int32_t N, int32_t C,
+                       int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias, float eps,
+                       int32_t relu, double* d_ws, float* d_save_mean, float* d_save_invstd, float* d_running_mean,
+                       float* d_running_var, float momentum, int64_t* d_num_batches_tracked, void* d_y,
+                       const double* d_part, int32_t nb_part, void* stream);
 int bb_bn_backward(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N,
                    int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                    const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
@@ -426,6 +435,12 @@ int bb_conv3x3_forward(const void* d_x, const void* d_w, int32_t N, int32_t cin,
  * gradient folded in (network.py:14-30). */
 int bb_conv3x3_forward_add(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout,
                            const void* d_add, void* d_y, void* stream);
+/* bb_conv3x3_forward that also writes, from its store pass, the following BatchNorm's batch-statistics
+ * partials: per workgroup and output channel the f64 sum and sum of squares of the stored bf16 outputs
+ * (d_part [bb_conv3x3_stats_blocks(N, cout)][cout][3], the third 0), for bb_bn_forward_part (ABI 8). */
+int32_t bb_conv3x3_stats_blocks(int32_t N, int32_t cout);
+int bb_conv3x3_forward_stats(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
+                             double* d_part, void* stream);
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
 /* bb_conv3x3_wgrad in two parts (ABI 8): the partial-sum kernel into d_ws, then the fixed-order sum of its

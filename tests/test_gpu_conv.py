@@ -345,3 +345,93 @@ def test_wgrad_piggyback_equals_plain(cuda, monkeypatch):
             K.Conv3x3Function.apply(xb, w).backward(dy)
         outs.append(w.grad)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cin,cout", SHAPES)
+@pytest.mark.parametrize("n", [1, 3, 257, 2048])
+def test_conv3x3_forward_stats(cuda, lib, cin, cout, n):
+    """bb_conv3x3_forward_stats: the same output as bb_conv3x3_forward (bit for bit) and, per workgroup and
+    channel, the sum and sum of squares of the stored bf16 outputs: their total within f32 summation noise of
+    the fp64 sums, the third slot 0."""
+    from runtime import kernels as K
+
+    x, w, _ = _inputs(cuda, n, cin, cout, 300 + n + cin + cout, layout=0)
+    y0 = K.Conv3x3Function.apply(x, w)
+    slot = K.StatsSlot()
+    y = K.Conv3x3Function.apply(x, w, None, None, slot)
+    assert torch.equal(y, y0)
+    assert slot.ptr == y.data_ptr() and slot.nb == lib.bb_conv3x3_stats_blocks(n, cout) == (n + 1) // 2
+    part = slot.part.view(slot.nb, cout, 3)
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, cout)
+    for m, ref in ((0, yd.sum(0)), (1, yd.square().sum(0))):
+        tot = part[:, :, m].sum(0)
+        scale = (yd.abs().sum(0) if m == 0 else yd.square().sum(0)).clamp_min(1e-30)
+        assert float(((tot - ref).abs() / scale).max()) < 1e-6, m
+    assert bool((part[:, :, 2] == 0).all())
+
+
+@pytest.mark.parametrize("res", [False, True])
+def test_bn_forward_from_conv_stats(cuda, lib, res):
+    """BatchNorm forward from the convolution's partials (bb_bn_forward_part) == its own reduction
+    (bb_bn_forward / _res): saved mean and inverse std within f64-vs-f32 summation noise, outputs within one
+    bf16 step (an element may round the other way), running statistics and num_batches_tracked alike."""
+    from runtime import kernels as K
+
+    n, c = 2048, 128
+    x, w, _ = _inputs(cuda, n, c, c, 77, layout=0)
+    slot = K.StatsSlot()
+    z = K.Conv3x3Function.apply(x, w, None, None, slot)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    pre_b, wt, bs = (torch.randn(c, device=cuda, generator=g) * 0.1 for _ in range(3))
+    wt = wt + 1.0
+    r = torch.randn_like(z.float()).bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for use in (slot, None):
+        rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+        nbt = torch.zeros((), dtype=torch.int64, device=cuda)
+        if res:
+            y = K.BatchNormAddReLUFunction.apply(z, pre_b, r, wt, bs, rm, rv, 0.1, 1e-5, nbt, None, use)
+        else:
+            y = K.BatchNormReLUFunction.apply(z, pre_b, wt, bs, rm, rv, 0.1, 1e-5, True, nbt, use)
+        outs.append((y, rm, rv, int(nbt)))
+    (y1, rm1, rv1, n1), (y2, rm2, rv2, n2) = outs
+    assert n1 == n2 == 1
+    assert torch.allclose(rm1, rm2, rtol=1e-5, atol=1e-6) and torch.allclose(rv1, rv2, rtol=1e-5, atol=1e-6)
+    step = (y2.float().abs() * 2.0 ** -7).clamp_min(2.0 ** -126)
+    assert bool(((y1.float() - y2.float()).abs() <= step).all())
+    assert float((y1 == y2).float().mean()) > 0.999
+
+
+def test_network_conv_stats_equals_own_reduction(cuda, monkeypatch):
+    """bf16 raw() forward + backward with the BatchNorm statistics from the convolutions' store passes ==
+    with the BatchNorms' own reduction passes: outputs within bf16 rounding, parameter gradients within 1%."""
+    import models.network as N
+    from runtime import kernels as K
+
+    torch.manual_seed(11)
+    net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
+    for mod in net.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    net.train()
+    x = (torch.rand((512, 4, 8, 8), device=cuda) < 0.4).float()
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(K, "CONV_STATS", on)
+        net.load_state_dict(state0)
+        net.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            lo, va = net.raw(x)
+        (lo.float().square().mean() + va.float().sum()).backward()
+        res[on] = (lo.detach().float(), va.detach().float(), {k: p.grad.clone() for k, p in net.named_parameters()},
+                   {k: b.clone() for k, b in net.named_buffers()})
+    assert torch.allclose(res[True][0], res[False][0], rtol=2.0 ** -6, atol=2e-3)
+    assert torch.allclose(res[True][1], res[False][1], rtol=2.0 ** -6, atol=2e-3)
+    for k, gr in res[True][2].items():
+        if k.endswith(".bias") and gr.dim() == 1 and res[True][2][k[:-5] + ".weight"].dim() == 4:
+            continue  # a conv bias before BatchNorm: zero up to noise
+        ref = res[False][2][k]
+        assert float((gr - ref).norm() / ref.norm().clamp_min(1e-30)) < 1e-2, k
+    for k, b in res[True][3].items():
+        assert torch.allclose(b.float(), res[False][3][k].float(), rtol=1e-4, atol=1e-6), k
