@@ -737,6 +737,31 @@ extern "C" int bb_bn_backward_red(const void* d_x, const void* d_dy, int32_t dty
   return BB_OK;
 }
 
+extern "C" int bb_bn_backward_part(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N,
+                                   int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
+                                   const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
+                                   int32_t relu, double* d_ws, void* d_dx, float* d_dweight, float* d_dbias,
+                                   float* d_dpre_bias, const float* d_conv_ws, int32_t conv_chunks, int32_t conv_cin,
+                                   int32_t conv_cout, int32_t conv_w_layout, float* d_conv_dw, const double* d_part,
+                                   int32_t nb_part, void* stream) {
+  int rc = bn_check(dtype, nhwc, N, C, HW);
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_dy || !d_weight || !d_bias || !d_save_mean || !d_save_invstd || !d_ws || !d_dx || !d_part ||
+      nb_part <= 0)
+    return fail(nullptr, BB_ERR_ARG, "bb_bn_backward_part: NULL argument");
+  if (reinterpret_cast<uintptr_t>(d_ws) % 16 != 0) return fail(nullptr, BB_ERR_ARG, "bb_bn: d_ws must be 16-byte aligned");
+  const bool red = d_conv_ws != nullptr;
+  if (red && (!d_conv_dw || conv_chunks <= 0 || (conv_w_layout != 0 && conv_w_layout != 1) ||
+              !conv3x3_supported(conv_cin, conv_cout)))
+    return fail(nullptr, BB_ERR_ARG, "bb_bn_backward_part: bad convolution reduction arguments");
+  const WgradReduceJob job{d_conv_ws, conv_chunks, conv_cout, conv_cin, conv_w_layout, d_conv_dw};
+  hipError_t st = launch_bn_backward(d_x, d_dy, dtype, nhwc, N, C, HW, d_pre_bias, d_weight, d_bias, d_save_mean,
+                                     d_save_invstd, relu, d_ws, d_dx, d_dweight, d_dbias, d_dpre_bias,
+                                     (hipStream_t)stream, nullptr, nullptr, red ? &job : nullptr, d_part, nb_part);
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_bn_backward_part");
+  return BB_OK;
+}
+
 extern "C" int bb_bn_backward_res(const void* d_x, const void* d_dy, const void* d_y, int32_t dtype, int32_t nhwc,
                                   int32_t N, int32_t C, int32_t HW, const float* d_pre_bias, const float* d_weight,
                                   const float* d_bias, const float* d_save_mean, const float* d_save_invstd,
@@ -912,10 +937,29 @@ extern "C" int bb_conv3x3_forward_stats(const void* d_x, const void* d_w, int32_
   if (!d_x || !d_w || !d_y || !d_part) return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: NULL argument");
   if (!al16(d_x) || !al16(d_w) || !al16(d_y))
     return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: tensors must be 16-byte aligned");
-  hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream, nullptr, d_part);
+  const ConvStatsArgs sa{d_part, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream, nullptr, &sa);
   if (st == hipErrorInvalidValue)
     return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_stats: not available in this (variant) build");
   if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward_stats");
+  return BB_OK;
+}
+
+extern "C" int bb_conv3x3_forward_bstats(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout,
+                                         void* d_y, const void* d_bn_x, const float* d_mean, const float* d_invstd,
+                                         const float* d_weight, const float* d_bias, int32_t relu, double* d_part,
+                                         void* stream) {
+  int rc = conv_check(N, cin, cout, "bb_conv3x3_forward_bstats");
+  if (rc != BB_OK) return rc;
+  if (!d_x || !d_w || !d_y || !d_part || !d_bn_x || !d_mean || !d_invstd || !d_weight || !d_bias)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_bstats: NULL argument");
+  if (!al16(d_x) || !al16(d_w) || !al16(d_y) || !al16(d_bn_x))
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_bstats: tensors must be 16-byte aligned");
+  const ConvStatsArgs sa{d_part, (const uint16_t*)d_bn_x, d_mean, d_invstd, d_weight, d_bias, relu ? 1 : 0};
+  hipError_t st = launch_conv3x3_forward(d_x, d_w, N, cin, cout, d_y, (hipStream_t)stream, nullptr, &sa);
+  if (st == hipErrorInvalidValue)
+    return fail(nullptr, BB_ERR_ARG, "bb_conv3x3_forward_bstats: not available in this (variant) build");
+  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_conv3x3_forward_bstats");
   return BB_OK;
 }
 

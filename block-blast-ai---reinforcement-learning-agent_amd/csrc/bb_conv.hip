@@ -210,17 +210,21 @@ __device__ __forceinline__ uint32_t add2_bf16(uint32_t a, uint32_t b) {  // two 
 // radd (NULL = none, shipped LDS-staged store path only): y = bf16(conv) + radd, rounded again -- the
 // data gradient of a ResidualBlock's first convolution plus the identity path's gradient, as autograd's
 // separate add kernel computed it
-// stats (NULL = none, same path, radd NULL): the following BatchNorm's batch statistics from the store pass --
-// per channel, the sum and the sum of squares of the stored bf16 outputs over the workgroup's pixels (f32 per
-// thread over its rows, the lanes of a channel by a fixed xor tree, the waves added in order in f64) ->
-// stats[(blockIdx.x * COUT + c) * 3 + {0, 1, 2 (= 0)}]: bn_reduce_nhwc's partial layout, so the BatchNorm
-// forward finalises from them without its own pass over the output (bb_bn_forward_part)
-template <int CIN, int COUT>
+// st.part (NULL = none, same path, radd NULL): BatchNorm reduction sums from the store pass, per channel over
+// the workgroup's pixels (f32 per thread over its rows, the lanes of a channel by a fixed xor tree, the waves
+// added in order in f64) -> st.part[(blockIdx.x * COUT + c) * 3 + q], bn_reduce_nhwc's partial layout:
+//   st.bx NULL: the following BatchNorm's forward statistics, q = {sum y, sum y^2, 0} of the stored bf16
+//               outputs (bb_bn_forward_part finalises from them without its own pass over y);
+//   st.bx set : this is a data gradient dy of a BatchNorm [+ ReLU] output whose input was st.bx (bf16, y's
+//               shape): q = {sum g, sum g xhat, sum xhat}, g = dy masked where the forward's ReLU was off,
+//               xhat = (x - mean) invstd -- bn_reduce_nhwc's backward arithmetic (bb_bn_backward_part).
+// BSTATS: the backward-statistics instantiation (st.bx set); the others carry none of its code.
+template <int CIN, int COUT, bool BSTATS = false>
 __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ y, int nb,
                                                                const uint16_t* __restrict__ radd,
-                                                               double* __restrict__ stats) {
+                                                               const ConvStatsArgs st) {
   constexpr int RB = CIN * 2;                 // bytes per pixel row
   constexpr int NCH = CIN / 8;                // 16-byte chunks per pixel row
   constexpr int FB = fwd_boards<COUT>();
@@ -400,7 +404,21 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
   // the output tile goes through LDS (free after the last stage's barrier) so that every global
   // store is a whole 16-byte chunk of a pixel row: row px of COUT bf16, 16-byte chunk c at c ^ (px & 15)
   constexpr int OCH = COUT / 8;  // 16-byte chunks per output row
+  constexpr int NIT = ROWS * OCH / kFwdThreads;  // store-pass chunks per thread
+  static_assert(ROWS * OCH % kFwdThreads == 0, "whole store-pass iterations");
   uint8_t* const os = sm;
+  // backward statistics: the BatchNorm input's chunks of this thread's store-pass positions, loaded now so
+  // their latency hides behind the tile's LDS staging
+  uint4 bxv[BSTATS ? NIT : 1];
+  if constexpr (BSTATS) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = tid + it * kFwdThreads, px = e / OCH, c = e % OCH;
+      bxv[it] = b0 + (px >> 6) < nb
+                    ? *reinterpret_cast<const uint4*>(st.bx + (size_t(b0) * 64 + px) * COUT + c * 8)
+                    : make_uint4(0, 0, 0, 0);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM16; ++i) {
     const int px = px0 + 16 * i + r16;
@@ -415,10 +433,28 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
   }
   __syncthreads();
   static_assert(kFwdThreads % OCH == 0, "a thread's output chunk column must stay fixed");
-  float ss[8], sq[8];  // stats: the 8 channels of chunk column tid % OCH
+  double* const stats = st.part;
+  constexpr bool bwd = BSTATS;
+  float ss[8], sq[8], sx[8];  // stats: the 8 channels of chunk column tid % OCH
+  float kmu[8], kis[8], ksc[8], ksh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ss[j] = sq[j] = 0.f;
-  for (int e = tid; e < ROWS * OCH; e += kFwdThreads) {
+  for (int j = 0; j < 8; ++j) {
+    ss[j] = sq[j] = sx[j] = 0.f;
+    kmu[j] = kis[j] = ksc[j] = ksh[j] = 0.f;
+  }
+  if (stats && bwd) {
+    const int c0 = (tid % OCH) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      kmu[j] = st.mean[c0 + j];
+      kis[j] = st.invstd[c0 + j];
+      ksc[j] = kis[j] * st.w[c0 + j];
+      ksh[j] = st.b[c0 + j];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * kFwdThreads;
     const int px = e / OCH, c = e % OCH;
     if (b0 + (px >> 6) >= nb) continue;
     if (BB_CONV_DIAG == 1 && acc[0][0][0] != 1.2345e-30f) continue;
@@ -430,13 +466,31 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
     }
     if (stats) {
       const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      float f[8];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float lo = __uint_as_float(vv[k] << 16), hi = __uint_as_float(vv[k] & 0xFFFF0000u);
-        ss[2 * k] += lo;
-        sq[2 * k] += lo * lo;
-        ss[2 * k + 1] += hi;
-        sq[2 * k + 1] += hi * hi;
+        f[2 * k] = __uint_as_float(vv[k] << 16);
+        f[2 * k + 1] = __uint_as_float(vv[k] & 0xFFFF0000u);
+      }
+      if constexpr (bwd) {
+        const uint4 xa = bxv[it];
+        const uint32_t xw[4] = {xa.x, xa.y, xa.z, xa.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xv = __uint_as_float((j & 1) ? (xw[j >> 1] & 0xFFFF0000u) : (xw[j >> 1] << 16));
+          const float u = xv + 0.f;  // bn_reduce's u = x + pb, pb = 0
+          const float g = (st.relu && (u - kmu[j]) * ksc[j] + ksh[j] <= 0.f) ? 0.f : f[j];  // the forward's ops
+          const float xh = (u - kmu[j]) * kis[j];
+          ss[j] += g;
+          sq[j] += g * xh;
+          sx[j] += xh;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ss[j] += f[j];
+          sq[j] += f[j] * f[j];
+        }
       }
     }
     *reinterpret_cast<uint4*>(y + o) = v;
@@ -448,22 +502,23 @@ __global__ void __launch_bounds__(kFwdThreads) conv_fwd_kernel(const uint16_t* _
       for (int m = OCH; m < 64; m <<= 1) {
         ss[j] += __shfl_xor(ss[j], m, 64);
         sq[j] += __shfl_xor(sq[j], m, 64);
+        sx[j] += __shfl_xor(sx[j], m, 64);
       }
-    float* red = reinterpret_cast<float*>(sm + ROWS * COUT * 2);  // past the output tile: [wave][2][COUT]
-    static_assert(ROWS * COUT * 2 + NW * 2 * COUT * 4 <= XBYTES + kFwdRing * WBYTES, "stats scratch");
+    float* red = reinterpret_cast<float*>(sm + ROWS * COUT * 2);  // past the output tile: [wave][3][COUT]
+    static_assert(ROWS * COUT * 2 + NW * 3 * COUT * 4 <= XBYTES + kFwdRing * WBYTES, "stats scratch");
     if (lane < OCH)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        red[(wid * 2 + 0) * COUT + lane * 8 + j] = ss[j];
-        red[(wid * 2 + 1) * COUT + lane * 8 + j] = sq[j];
+        red[(wid * 3 + 0) * COUT + lane * 8 + j] = ss[j];
+        red[(wid * 3 + 1) * COUT + lane * 8 + j] = sq[j];
+        red[(wid * 3 + 2) * COUT + lane * 8 + j] = sx[j];
       }
     __syncthreads();
     for (int t = tid; t < COUT * 3; t += kFwdThreads) {
       const int c = t / 3, m = t % 3;
       double a = 0.0;
-      if (m < 2)
 #pragma unroll
-        for (int wv = 0; wv < NW; ++wv) a += (double)red[(wv * 2 + m) * COUT + c];
+      for (int wv = 0; wv < NW; ++wv) a += (double)red[(wv * 3 + m) * COUT + c];
       stats[(size_t)blockIdx.x * COUT * 3 + t] = a;
     }
   }
@@ -836,13 +891,18 @@ int wgrad_bpc(int nb, int nchunk) {
 }
 
 template <int CIN, int COUT>
-hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd = nullptr,
-                 double* stats = nullptr) {
-  if (nb <= 0 || (radd && stats)) return hipErrorInvalidValue;
+hipError_t fwd_t(const void* x, const void* w, int nb, void* y, hipStream_t s, const void* radd,
+                 const ConvStatsArgs& st) {
+  if (nb <= 0 || (radd && st.part)) return hipErrorInvalidValue;
   // variant builds: no fused add / statistics
-  if ((radd || stats) && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), dim3((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>()), dim3(kFwdThreads), 0, s,
-                     (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd, stats);
+  if ((radd || st.part) && !(BB_CONV_MFMA16 && BB_CONV_STORE_LDS)) return hipErrorInvalidValue;
+  const dim3 grid((nb + fwd_boards<COUT>() - 1) / fwd_boards<COUT>());
+  if (st.part && st.bx)
+    hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT, true>), grid, dim3(kFwdThreads), 0, s, (const uint16_t*)x,
+                       (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd, st);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<CIN, COUT>), grid, dim3(kFwdThreads), 0, s, (const uint16_t*)x,
+                       (const uint16_t*)w, (uint16_t*)y, nb, (const uint16_t*)radd, st);
   return hipGetLastError();
 }
 
@@ -1160,11 +1220,13 @@ hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int
 }
 
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
-                                  const void* radd, double* stats) {
-  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s, radd, stats);
-  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd, stats);
-  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd, stats);
-  return fwd_t<128, 128>(x, w, nb, y, s, radd, stats);
+                                  const void* radd, const ConvStatsArgs* stats) {
+  ConvStatsArgs st{};
+  if (stats) st = *stats;
+  if (cin == 64 && cout == 64) return fwd_t<64, 64>(x, w, nb, y, s, radd, st);
+  if (cin == 64 && cout == 128) return fwd_t<64, 128>(x, w, nb, y, s, radd, st);
+  if (cin == 128 && cout == 64) return fwd_t<128, 64>(x, w, nb, y, s, radd, st);
+  return fwd_t<128, 128>(x, w, nb, y, s, radd, st);
 }
 
 int conv3x3_stats_blocks(int nb, int cout) {

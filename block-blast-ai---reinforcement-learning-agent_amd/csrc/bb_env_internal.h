@@ -117,15 +117,28 @@ struct WgradReduceJob {  // conv_wgrad_reduce's arguments
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
                               int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s,
-                              const void* mask = nullptr, void* gout = nullptr, const WgradReduceJob* job = nullptr);
+                              const void* mask = nullptr, void* gout = nullptr, const WgradReduceJob* job = nullptr,
+                              const double* ext_part = nullptr, int ext_nb = 0);
 
 bool conv3x3_supported(int cin, int cout);
 int64_t conv3x3_wgrad_workspace_bytes(int nb, int cin, int cout);
 hipError_t launch_conv3x3_prep(const float* w, int cin, int cout, int wl, void* wf, void* wd, hipStream_t s);
 hipError_t launch_conv3x3_prep_multi(int count, const float* const* w, const int32_t* cin, const int32_t* cout,
                                      const int32_t* wl, void* const* wf, void* const* wd, hipStream_t s);
+// BatchNorm reduction sums from a board convolution's store pass (conv_fwd_kernel): part [blocks][cout][3];
+// bx NULL: forward statistics of the output, else the output is a BatchNorm's output gradient and bx, mean,
+// invstd, w, b, relu that BatchNorm's input and forward coefficients
+struct ConvStatsArgs {
+  double* part;
+  const uint16_t* bx;
+  const float* mean;
+  const float* invstd;
+  const float* w;
+  const float* b;
+  int relu;
+};
 hipError_t launch_conv3x3_forward(const void* x, const void* w, int nb, int cin, int cout, void* y, hipStream_t s,
-                                  const void* radd = nullptr, double* stats = nullptr);
+                                  const void* radd = nullptr, const ConvStatsArgs* stats = nullptr);
 int conv3x3_stats_blocks(int nb, int cout);
 hipError_t launch_conv3x3_wgrad(const void* x, const void* dy, int nb, int cin, int cout, float* ws, int wl,
                                 float* dw, hipStream_t s);

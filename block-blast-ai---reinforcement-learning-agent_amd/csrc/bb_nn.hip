@@ -603,12 +603,16 @@ template <typename T>
 hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, int HW, const float* pb,
                          const float* w, const float* b, const float* mean, const float* invstd, int relu, double* ws,
                          void* dx, float* dw, float* db, float* dpb, hipStream_t s, const void* mask, void* gout,
-                         const WgradReduceJob* job) {
+                         const WgradReduceJob* job, const double* ext_part, int ext_nb) {
   const Plan p = plan_for(sizeof(T), nhwc, N, C, HW);
   const Ws k = split_ws(ws, C);
   // with a mask (the ResidualBlock tail): the reduction writes the masked gradient g to gout, and the
-  // elementwise pass reads g as its dy (no mask there)
-  launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s, mask, gout);
+  // elementwise pass reads g as its dy (no mask there).  ext_part (no mask): the reduction's partials came
+  // from the board convolution that produced dy (conv_fwd_kernel's backward statistics)
+  if (ext_part && mask) return hipErrorInvalidValue;
+  const double* part = ext_part ? ext_part : k.part;
+  const int nbp = ext_part ? ext_nb : p.nb;
+  if (!ext_part) launch_reduce<T, true>(p, nhwc, x, dy, N, C, HW, pb, w, b, mean, invstd, relu, k.part, s, mask, gout);
   if (mask) dy = gout;
   WgradReduceJob jb{};
   int red_blocks = 0;
@@ -616,7 +620,7 @@ hipError_t bn_backward_t(const void* x, const void* dy, int nhwc, int N, int C, 
     jb = *job;
     red_blocks = (9 * jb.cout * jb.cin + kBnThreads - 1) / kBnThreads;
   }
-  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kFinCpb - 1) / kFinCpb + red_blocks), dim3(kBnThreads), 0, s, k.part, p.nb, C,
+  hipLaunchKernelGGL(bn_finalize_bwd, dim3((C + kFinCpb - 1) / kFinCpb + red_blocks), dim3(kBnThreads), 0, s, part, nbp, C,
                      (double)N * HW, pb, w, b, mean, invstd, dw, db, dpb, k.coef, jb);
   const dim3 ge(grid_for_elems(p.chunks, nhwc));
   if (nhwc)
@@ -649,12 +653,13 @@ hipError_t launch_bn_forward(const void* x, const void* res, int dtype, int nhwc
 hipError_t launch_bn_backward(const void* x, const void* dy, int dtype, int nhwc, int N, int C, int HW,
                               const float* pb, const float* w, const float* b, const float* mean, const float* invstd,
                               int relu, double* ws, void* dx, float* dw, float* db, float* dpb, hipStream_t s,
-                              const void* mask, void* gout, const WgradReduceJob* job) {
+                              const void* mask, void* gout, const WgradReduceJob* job, const double* ext_part,
+                              int ext_nb) {
   if (dtype == 1)
     return bn_backward_t<__hip_bfloat16>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s,
-                                         mask, gout, job);
+                                         mask, gout, job, ext_part, ext_nb);
   return bn_backward_t<float>(x, dy, nhwc, N, C, HW, pb, w, b, mean, invstd, relu, ws, dx, dw, db, dpb, s, mask, gout,
-                              job);
+                              job, ext_part, ext_nb);
 }
 
 }  // namespace bb

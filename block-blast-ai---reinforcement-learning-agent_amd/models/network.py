@@ -41,16 +41,19 @@ class BatchNorm2d(nn.BatchNorm2d):
 
         return bn_fusable(x)
 
-    def forward(self, x: torch.Tensor, pre_bias: Optional[torch.Tensor] = None, stats=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, pre_bias: Optional[torch.Tensor] = None, stats=None,
+                bwd_slot=None) -> torch.Tensor:
         """BatchNorm2d(x + pre_bias) [-> ReLU]; ``pre_bias`` is a preceding
         convolution's bias that was left out of the convolution; ``stats`` its
-        runtime.kernels.StatsSlot (the batch statistics from its store pass)."""
+        runtime.kernels.StatsSlot (the batch statistics from its store pass);
+        ``bwd_slot`` the slot of the convolution reading this output (its data
+        gradient's store pass makes this backward's reduction sums)."""
         if self.fusable(x):
             from runtime.kernels import BatchNormReLUFunction
 
             return BatchNormReLUFunction.apply(x, pre_bias, self.weight, self.bias, self.running_mean,
                                                self.running_var, self.momentum, self.eps, self.fuse_relu,
-                                               self.num_batches_tracked, stats)  # += 1 in the finalize kernel
+                                               self.num_batches_tracked, stats, bwd_slot)  # nbt += 1 on device
         if pre_bias is not None:
             x = x + pre_bias.view(1, -1, 1, 1).to(x.dtype)
         y = super().forward(x)
@@ -108,7 +111,8 @@ def _hip_conv_on(x: torch.Tensor) -> bool:
         and torch.get_autocast_dtype("cuda") == torch.bfloat16
 
 
-def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None, stats=None) -> torch.Tensor:
+def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None, stats=None,
+                bwd_slot=None) -> torch.Tensor:
     """conv(x) without its bias.  Under bf16 autocast on the GPU the 3x3
     layers with 64 or 128 channels in and out run on the HIP kernels
     (runtime.kernels.Conv3x3Function): bf16 NHWC, f32 accumulation, as
@@ -121,7 +125,8 @@ def conv_nobias(conv: nn.Conv2d, x: torch.Tensor, images=None, mailbox=None, sta
         if conv3x3_fusable(x, conv):
             if prep is not None:
                 prep.run()
-            return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox, stats)
+            return Conv3x3Function.apply(x, conv.weight, images.get(conv) if images else None, mailbox, stats,
+                                         bwd_slot)
         if conv_in_fusable(x, conv):  # the 4 -> 64 input layer: f32 boards in, bf16 NHWC out (+ the images)
             return ConvInFunction.apply(x, conv.weight, prep)
     elif _f32_conv_on(x, conv):
@@ -140,7 +145,8 @@ def _stats_slot(x: torch.Tensor):
     return StatsSlot()
 
 
-def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None, mailbox=None) -> torch.Tensor:
+def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None, mailbox=None,
+            bwd_slot=None) -> torch.Tensor:
     """bn(conv(x)).  When the BatchNorm runs on the HIP kernels the
     convolution's bias is added inside them (one add on load instead of a
     separate pass, and its gradient comes out of the BatchNorm backward instead
@@ -149,7 +155,7 @@ def conv_bn(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, images=None, mailbo
         slot = _stats_slot(x)
         z = conv_nobias(conv, x, images, mailbox, slot)
         if bn.fusable(z):
-            return bn(z, pre_bias=conv.bias, stats=slot)
+            return bn(z, pre_bias=conv.bias, stats=slot, bwd_slot=bwd_slot)
         return bn(z + conv.bias.view(1, -1, 1, 1).to(z.dtype))
     return bn(conv(x))
 
@@ -194,10 +200,11 @@ class ResidualBlock(nn.Module):
 
             if conv3x3_fusable(x, self.conv1):  # conv1's data gradient adds the identity path's gradient
                 mailbox = GradMailbox()
-        y = conv_bn(self.conv1, self.bn1, x, images, mailbox)
+        bslot = _stats_slot(x)  # bn1's backward sums from conv2's data-gradient store pass
+        y = conv_bn(self.conv1, self.bn1, x, images, mailbox, bslot)
         if fused:
             slot = _stats_slot(y)
-            z = conv_nobias(conv2, y, images, None, slot)
+            z = conv_nobias(conv2, y, images, None, slot, bslot)
             from runtime.kernels import BatchNormAddReLUFunction, _bn_layout
 
             if bn2.fusable(z) and x.dtype == z.dtype and x.shape == z.shape and _bn_layout(x) == _bn_layout(z):

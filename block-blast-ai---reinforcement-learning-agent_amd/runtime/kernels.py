@@ -157,15 +157,22 @@ def bn_fusable(x: torch.Tensor) -> bool:
 # BatchNorm batch statistics from the producing convolution's store pass (bb_conv3x3_forward_stats ->
 # bb_bn_forward_part): no reduction pass over the convolution's output (0: bb_bn_forward's own pass, for A/B)
 CONV_STATS = os.environ.get("BB_CONV_STATS", "1") != "0"
+# ... and a ResidualBlock's bn1 backward sums from conv2's data-gradient store pass (bb_conv3x3_forward_bstats).
+# Off: 1.510 against 1.503 ms per update step (the store pass's +11.5 us per launch outweighs the 13.6 us
+# reduction it replaces plus the extra partials; profiles/r05/ab/convstats)
+CONV_BSTATS = os.environ.get("BB_CONV_BSTATS", "0") != "0"
 
 
 class StatsSlot:
-    """Carries bb_conv3x3_forward_stats' partials from a board convolution to the BatchNorm reading its output."""
+    """Carries BatchNorm reduction partials from a board convolution's store pass to a BatchNorm: forward, the
+    statistics of the convolution's output (bb_conv3x3_forward_stats); backward, the reduction sums of the
+    BatchNorm whose output the convolution read, from the convolution's data gradient
+    (bb_conv3x3_forward_bstats; ``bn`` = that BatchNorm's input and coefficients, set by its forward)."""
 
-    __slots__ = ("part", "nb", "ptr")
+    __slots__ = ("part", "nb", "ptr", "bn")
 
     def __init__(self):
-        self.part, self.nb, self.ptr = None, 0, 0
+        self.part, self.nb, self.ptr, self.bn = None, 0, 0, None
 
 
 def _stats_for(slot, x: torch.Tensor):
@@ -184,15 +191,21 @@ def _bn_workspace(x: torch.Tensor, nhwc: int) -> torch.Tensor:
     return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=x.device)
 
 
-def _bn_backward_call(x, dy, nhwc, pre_bias, weight, bias, mean, invstd, relu: int, ws, dx, dw, db, dpb, dev):
+def _bn_backward_call(x, dy, nhwc, pre_bias, weight, bias, mean, invstd, relu: int, ws, dx, dw, db, dpb, dev,
+                      part=None):
     """bb_bn_backward, or bb_bn_backward_red carrying a board convolution's pending weight-gradient reduction
-    (wgrad_piggyback) in its finalisation launch."""
+    (wgrad_piggyback) in its finalisation launch; part = (partials, blocks): bb_bn_backward_part (the reduction
+    sums from the convolution that produced dy)."""
     n, c, h, w = x.shape
     lib = L.load()
     job = _take_pending_reduce(dev)
     args = (_p(x), _p(dy), _BN_DTYPES[x.dtype], nhwc, n, c, h * w, _p(pre_bias), _p(weight), _p(bias), _p(mean),
             _p(invstd), int(relu), _p(ws), _p(dx), _p(dw), _p(db), _p(dpb))
-    if job is None:
+    if part is not None:
+        cws, chunks, cin, cout, wl, cdw = job if job is not None else (None, 0, 0, 0, 0, None)
+        L.check(lib.bb_bn_backward_part(*args, _p(cws), chunks, cin, cout, wl, C.c_void_p(cdw), _p(part[0]), part[1],
+                                        _s(dev)), "bb_bn_backward_part")
+    elif job is None:
         L.check(lib.bb_bn_backward(*args, _s(dev)), "bb_bn_backward")
     else:
         cws, chunks, cin, cout, wl, cdw = job
@@ -209,7 +222,7 @@ class BatchNormReLUFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, pre_bias, weight, bias, running_mean, running_var, momentum: float, eps: float, relu: bool,
-                num_batches_tracked=None, stats=None):
+                num_batches_tracked=None, stats=None, bwd_slot=None):
         nhwc = _bn_layout(x)
         x = x.contiguous(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
         n, c, h, w = x.shape
@@ -230,6 +243,10 @@ class BatchNormReLUFunction(torch.autograd.Function):
         ctx.save_for_backward(x, pre_bias, weight, bias, mean, invstd)
         ctx.relu = bool(relu)
         ctx.nhwc = nhwc
+        ctx.bwd_slot = None
+        if bwd_slot is not None and nhwc and x.dtype == torch.bfloat16:  # for the next convolution's backward
+            bwd_slot.bn = (x, weight, bias, mean, invstd, int(relu))
+            ctx.bwd_slot = bwd_slot
         return y
 
     @staticmethod
@@ -244,9 +261,13 @@ class BatchNormReLUFunction(torch.autograd.Function):
         db = torch.empty_like(bias)
         dpb = torch.empty_like(pre_bias) if pre_bias is not None else None
         ws = _bn_workspace(x, ctx.nhwc)
+        slot = ctx.bwd_slot
+        part = _stats_for(slot, dy)
+        if slot is not None:
+            slot.part, slot.bn = None, None  # used once
         _bn_backward_call(x, dy, ctx.nhwc, pre_bias, weight, bias, mean, invstd, int(ctx.relu), ws, dx, dw, db, dpb,
-                          dev)
-        return dx, dpb, dw, db, None, None, None, None, None, None, None
+                          dev, part)
+        return dx, dpb, dw, db, None, None, None, None, None, None, None, None
 
 
 # ResidualBlock tail backward on bb_bn_backward_res: the ReLU mask applied in the BatchNorm reduction, which
@@ -526,9 +547,10 @@ class Conv3x3Function(torch.autograd.Function):
     kernel over dy with the tap-reversed, transposed weight image)."""
 
     @staticmethod
-    def forward(ctx, x, weight, images=None, grad_mailbox=None, stats=None):
+    def forward(ctx, x, weight, images=None, grad_mailbox=None, stats=None, bwd_slot=None):
         _need_cuda(x, weight)
         ctx.mailbox = grad_mailbox
+        ctx.bwd_slot = bwd_slot
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n, cin = x.shape[0], x.shape[1]
         cout = weight.shape[0]
@@ -570,8 +592,21 @@ class Conv3x3Function(torch.autograd.Function):
                 L.check(lib.bb_conv3x3_forward_add(_p(dy), _p(wd), n, cout, cin, _p(extra), _p(dx), _s(dev)),
                         "bb_conv3x3_forward_add")
             else:
-                L.check(lib.bb_conv3x3_forward(_p(dy), _p(wd), n, cout, cin, _p(dx), _s(dev)),
-                        "bb_conv3x3_forward")
+                slot = ctx.bwd_slot
+                bn = slot.bn if slot is not None and CONV_STATS and CONV_BSTATS else None
+                if bn is not None and bn[0].shape == dx.shape and bn[0].dtype == torch.bfloat16 \
+                        and bn[0].is_contiguous(memory_format=torch.channels_last):
+                    # + the reduction sums of the BatchNorm whose output x is (its backward skips its own pass)
+                    nbp = lib.bb_conv3x3_stats_blocks(n, cin)
+                    part = torch.empty(nbp * cin * 3, dtype=torch.float64, device=dev)
+                    bx, bw, bb, bmean, binv, brelu = bn
+                    L.check(lib.bb_conv3x3_forward_bstats(_p(dy), _p(wd), n, cout, cin, _p(dx), _p(bx), _p(bmean),
+                                                          _p(binv), _p(bw), _p(bb), brelu, _p(part), _s(dev)),
+                            "bb_conv3x3_forward_bstats")
+                    slot.part, slot.nb, slot.ptr = part, nbp, dx.data_ptr()
+                else:
+                    L.check(lib.bb_conv3x3_forward(_p(dy), _p(wd), n, cout, cin, _p(dx), _s(dev)),
+                            "bb_conv3x3_forward")
         if ctx.needs_input_grad[1]:
             nbytes = lib.bb_conv3x3_workspace_bytes(n, cin, cout)
             if nbytes < 0:
@@ -598,7 +633,7 @@ class Conv3x3Function(torch.autograd.Function):
                 st[2].append((weight, dw.data_ptr()))
             elif not _wgrad_deferred(weight, dev, (x, dy), wgrad):
                 dw = wgrad()
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 _CONV32_PAIRS = ((128, 128), (64, 128))  # forward layers; the 64 -> 128 layer's data gradient runs (128, 64)

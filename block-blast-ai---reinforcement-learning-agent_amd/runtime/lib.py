@@ -146,6 +146,8 @@ SIGNATURES = {
                                 _P]),
     "bb_bn_forward_res": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P,
                                     _F, _P, _P, _P]),
+    "bb_bn_backward_part": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P,
+                                      _P, _P, _I32, _I32, _I32, _I32, _P, _P, _I32, _P]),
     "bb_bn_forward_part": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _I32, _P, _P, _P, _P, _P,
                                      _F, _P, _P, _P, _I32, _P]),
     "bb_bn_backward": (C.c_int, [_P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P,
@@ -161,6 +163,7 @@ SIGNATURES = {
     "bb_conv3x3_forward_add": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
     "bb_conv3x3_stats_blocks": (C.c_int32, [_I32, _I32]),
     "bb_conv3x3_forward_stats": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
+    "bb_conv3x3_forward_bstats": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P, _P]),
     "bb_conv3x3_wgrad": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _I32, _P, _P]),
     "bb_conv3x3_wgrad_chunks": (C.c_int32, [_I32, _I32, _I32]),
     "bb_conv3x3_wgrad_partial": (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),

@@ -43,7 +43,8 @@ extern "C" {
                                  loss forward's d_cnt (one launch, the statistics finalised in it);
                                  bb_conv3x3_wgrad_partial / _reduce / _chunks, bb_bn_backward_red,
                                  bb_conv_in_forward_prep, bb_linear_bgrad2, bb_conv3x3_forward_stats,
-                                 bb_conv3x3_stats_blocks, bb_bn_forward_part */
+                                 bb_conv3x3_stats_blocks, bb_bn_forward_part, bb_conv3x3_forward_bstats,
+                                 bb_bn_backward_part */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -348,6 +349,15 @@ int bb_bn_backward_red(const void* d_x, const void* d_dy, int32_t dtype, int32_t
                        const float* d_save_invstd, int32_t relu, double* d_ws, void* d_dx, float* d_dweight,
                        float* d_dbias, float* d_dpre_bias, const float* d_conv_ws, int32_t conv_chunks,
                        int32_t conv_cin, int32_t conv_cout, int32_t conv_w_layout, float* d_conv_dw, void* stream);
+/* bb_bn_backward / _red from reduction partials the board convolution that produced d_dy already made
+ * (bb_conv3x3_forward_bstats: d_part [nb_part][C][3] doubles) instead of its own pass over x and dy; d_conv_ws
+ * NULL: no carried weight-gradient reduction (ABI 8). */
+int bb_bn_backward_part(const void* d_x, const void* d_dy, int32_t dtype, int32_t nhwc, int32_t N, int32_t C,
+                        int32_t HW, const float* d_pre_bias, const float* d_weight, const float* d_bias,
+                        const float* d_save_mean, const float* d_save_invstd, int32_t relu, double* d_ws, void* d_dx,
+                        float* d_dweight, float* d_dbias, float* d_dpre_bias, const float* d_conv_ws,
+                        int32_t conv_chunks, int32_t conv_cin, int32_t conv_cout, int32_t conv_w_layout,
+                        float* d_conv_dw, const double* d_part, int32_t nb_part, void* stream);
 /* The backward of bb_bn_forward_res with its ReLU: bb_bn_backward (relu = 0) over g = (y > 0 ? dy : 0), y the
  * forward's output (torch's threshold_backward): the reduction pass applies the mask and writes g to d_gres (x's
  * shape, dtype and layout; required), the elementwise pass reads it -- three launches, as bb_bn_backward, and no
@@ -441,6 +451,13 @@ int bb_conv3x3_forward_add(const void* d_x, const void* d_w, int32_t N, int32_t 
 int32_t bb_conv3x3_stats_blocks(int32_t N, int32_t cout);
 int bb_conv3x3_forward_stats(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
                              double* d_part, void* stream);
+/* bb_conv3x3_forward run as a data gradient (y = dL/d(BatchNorm [+ ReLU] output)) that also writes that
+ * BatchNorm's backward reduction partials: per workgroup and channel {sum g, sum g xhat, sum xhat}, g = y where
+ * the forward's ReLU (relu != 0) passed, xhat = (bn_x - mean) invstd, bn_x the BatchNorm's bf16 NHWC input
+ * (y's shape) and mean / invstd / weight / bias its forward's (bb_bn_backward_part; ABI 8). */
+int bb_conv3x3_forward_bstats(const void* d_x, const void* d_w, int32_t N, int32_t cin, int32_t cout, void* d_y,
+                              const void* d_bn_x, const float* d_mean, const float* d_invstd, const float* d_weight,
+                              const float* d_bias, int32_t relu, double* d_part, void* stream);
 int bb_conv3x3_wgrad(const void* d_x, const void* d_dy, int32_t N, int32_t cin, int32_t cout, float* d_ws,
                      int32_t w_layout, float* d_dw, void* stream);
 /* bb_conv3x3_wgrad in two parts (ABI 8): the partial-sum kernel into d_ws, then the fixed-order sum of its

@@ -402,11 +402,15 @@ def test_bn_forward_from_conv_stats(cuda, lib, res):
     assert float((y1 == y2).float().mean()) > 0.999
 
 
-def test_network_conv_stats_equals_own_reduction(cuda, monkeypatch):
-    """bf16 raw() forward + backward with the BatchNorm statistics from the convolutions' store passes ==
-    with the BatchNorms' own reduction passes: outputs within bf16 rounding, parameter gradients within 1%."""
+@pytest.mark.parametrize("bstats", [False, True])
+def test_network_conv_stats_equals_own_reduction(cuda, monkeypatch, bstats):
+    """bf16 raw() forward + backward with the BatchNorm statistics (and, bstats, bn1's backward sums) from the
+    convolutions' store passes == with the BatchNorms' own reduction passes: outputs within bf16 rounding,
+    parameter gradients within 1%."""
     import models.network as N
     from runtime import kernels as K
+
+    monkeypatch.setattr(K, "CONV_BSTATS", bstats)
 
     torch.manual_seed(11)
     net = N.BlockBlastNetwork().to(cuda).to(memory_format=torch.channels_last)
@@ -435,3 +439,41 @@ def test_network_conv_stats_equals_own_reduction(cuda, monkeypatch):
         assert float((gr - ref).norm() / ref.norm().clamp_min(1e-30)) < 1e-2, k
     for k, b in res[True][3].items():
         assert torch.allclose(b.float(), res[False][3][k].float(), rtol=1e-4, atol=1e-6), k
+
+
+@pytest.mark.parametrize("c,n,relu", [(128, 2048, 1), (64, 257, 1), (128, 3, 0)])
+def test_conv3x3_forward_bstats(cuda, lib, c, n, relu):
+    """bb_conv3x3_forward_bstats: the data gradient bit-identical to bb_conv3x3_forward, and per workgroup and
+    channel the BatchNorm backward sums {sum g, sum g xhat, sum xhat} of the stored bf16 gradient, g masked
+    where the forward's ReLU was off (the same f32 operations), within f32 summation noise of fp64."""
+    from runtime import kernels as K
+
+    x, w, dy = _inputs(cuda, n, c, c, 500 + n + c, layout=0)
+    g0 = torch.Generator(device=cuda).manual_seed(n)
+    bx = torch.randn((n, c, 8, 8), device=cuda, generator=g0).bfloat16().contiguous(memory_format=torch.channels_last)
+    mean = torch.randn(c, device=cuda, generator=g0) * 0.1
+    invstd = torch.rand(c, device=cuda, generator=g0) + 0.5
+    bw = torch.randn(c, device=cuda, generator=g0) * 0.2 + 1.0
+    bb = torch.randn(c, device=cuda, generator=g0) * 0.1
+    wf = torch.empty(9 * c * c, dtype=torch.bfloat16, device=cuda)
+    wd = torch.empty_like(wf)
+    L_ = K.L
+    L_.check(lib.bb_conv3x3_prep(K._p(w), c, c, 0, K._p(wf), K._p(wd), K._s(cuda)), "prep")
+    y0 = torch.empty_like(x)
+    y = torch.empty_like(x)
+    L_.check(lib.bb_conv3x3_forward(K._p(dy), K._p(wd), n, c, c, K._p(y0), K._s(cuda)), "fwd")
+    nbp = lib.bb_conv3x3_stats_blocks(n, c)
+    part = torch.empty(nbp * c * 3, dtype=torch.float64, device=cuda)
+    L_.check(lib.bb_conv3x3_forward_bstats(K._p(dy), K._p(wd), n, c, c, K._p(y), K._p(bx), K._p(mean), K._p(invstd),
+                                           K._p(bw), K._p(bb), relu, K._p(part), K._s(cuda)), "bstats")
+    assert torch.equal(y, y0)
+    u = bx.float().permute(0, 2, 3, 1).reshape(-1, c)
+    gy = y.float().permute(0, 2, 3, 1).reshape(-1, c)
+    sc = invstd * bw
+    off = ((u - mean) * sc + bb) <= 0 if relu else torch.zeros_like(u, dtype=torch.bool)
+    g = torch.where(off, torch.zeros_like(gy), gy).double()
+    xh = ((u - mean) * invstd).double()
+    tot = part.view(nbp, c, 3).sum(0)
+    for m, ref, scale in ((0, g.sum(0), g.abs().sum(0)), (1, (g * xh).sum(0), (g * xh).abs().sum(0)),
+                          (2, xh.sum(0), xh.abs().sum(0))):
+        assert float(((tot[:, m] - ref).abs() / scale.clamp_min(1e-30)).max()) < 1e-5, m
