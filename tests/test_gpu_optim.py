@@ -94,10 +94,11 @@ def test_adam_clip_rejects_bad_tables(cuda):
 def test_cast_multi_exact(cuda):
     from runtime import kernels as K
 
-    src = _tensors(cuda, 7, shapes=[(512, 8192), (512,), (3,), (2051,), (192, 256), (4, 64)], channels_last=False)
+    src = _tensors(cuda, 7, shapes=[(512, 8192), (512,), (3,), (2051,), (192, 256), (4, 64), (3, 60)],
+                   channels_last=False)
     src[0] *= 1e-3
     src[1][:4] = torch.tensor([float("inf"), float("-inf"), float("nan"), 1.0 + 2 ** -8], device=cuda)
-    perms = [(128, 64), (0, 0), (0, 0), (0, 0), (0, 0), (16, 4)]
+    perms = [(128, 64), (0, 0), (0, 0), (0, 0), (0, 0), (16, 4), (12, 5)]  # (12, 5): the scalar permute
     out = [torch.empty(s.shape, dtype=torch.bfloat16, device=cuda) for s in src]
     K.cast_multi(0, src, out, perms)
 
