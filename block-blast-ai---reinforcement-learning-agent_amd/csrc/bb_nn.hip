@@ -325,7 +325,9 @@ template <int NQR>
 __device__ __forceinline__ bool channel_sums_block(const double* __restrict__ part, int nb, int C, int& c,
                                                    double a[kQ]) {
   __shared__ double red[kQ][kBnThreads / 64];
-  c = blockIdx.x;
+  // blocks b, b + 8, ... share an XCD (round-robin dealing, MI355X_MICROARCH.md): give them consecutive
+  // channels, so the partial rows' cache lines (5 channels per 128 B) are fetched into one L2, not eight
+  c = (C % 8 == 0 && (int)gridDim.x >= C) ? ((int)blockIdx.x % 8) * (C / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
   a[0] = a[1] = a[2] = 0.0;
   int blk = threadIdx.x;
   for (; blk + kBnThreads < nb; blk += 2 * kBnThreads) {  // two rows' loads in flight
