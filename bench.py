@@ -16,8 +16,15 @@ counts env-steps (envs x T x K in rollout mode, envs x K in step mode) over
 the timed wall time.
 
     python bench.py --gpus N --steps K --warmup W [--mode rollout|step]
-    (N > 1: launched by torch.distributed.run, one rank per GPU; envs are
-     independent shards, no collective on the data path -> weak scaling)
+    (N > 1: one rank per GPU; run under torch.distributed.run, or plain
+     `python bench.py --gpus N`, which starts torch.distributed.run itself as a
+     child process before any GPU call and exits with its code.  Envs are
+     independent shards, no collective on the data path -> weak scaling.
+     After the env timing every rank also runs the `dp_update` leg: PPO
+     optimizer steps on its own 2,048-sample minibatches (BASELINE configs 4
+     fp32 and 5 bf16, minibatch_scope per_gpu) with the RCCL gradient
+     all-reduce of /root/reference/src/agents/ppo.py:395-401's optimizer step,
+     timed beside the same step without the collective)
 
 Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel
 against HBM with the algorithmic bytes of SURVEY.md 8(d) (194 B per env-step)
@@ -62,10 +69,10 @@ def host_facts() -> dict:
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def load_valu(n_envs: int, steps_per_launch: int):
+def load_valu(n_envs: int, steps_per_launch: int, build_id: str):
     """The rollout kernel's instruction-issue record (its binding resource) from a committed
     rocprofv3 SQ-counter run (profiles/sq_rollout_kernel.json, tools/sq_summary.py --json), or None when it
-    was taken on another shape."""
+    was taken on another shape or on a library built from other sources than the loaded one."""
     p = os.path.join(REPO, "profiles", "sq_rollout_kernel.json")
     try:
         with open(p) as f:
@@ -73,6 +80,8 @@ def load_valu(n_envs: int, steps_per_launch: int):
     except (OSError, ValueError):
         return None
     if int(d.get("n_envs", -1)) != n_envs or int(d.get("steps_per_launch", -1)) != steps_per_launch:
+        return None
+    if d.get("build_id") != build_id:
         return None
     keys = ("valu_insts_per_launch", "valu_insts_per_env_step", "wave_cycles_per_env_step",
             "cycles_per_valu_per_simd", "issue_floor_cycles", "issue_frac", "profiled_ms", "build_id")
@@ -159,20 +168,137 @@ def cpu_baseline_native(seconds: float = 8.0, n: int = 65536, T: int = 16) -> di
     }
 
 
-def load_traffic(n_envs: int, mode: str, steps_per_launch: int):
+def load_traffic(n_envs: int, mode: str, steps_per_launch: int, build_id: str):
     """HBM bytes per launch from a committed rocprofv3 PMC run
     (profiles/pmc_step_kernel.json or pmc_rollout_kernel.json, written by
     tools/pmc_traffic.py from two separate --pmc passes, FETCH_SIZE doubled
-    per the gfx950 note), or None when it was taken on another shape."""
+    per the gfx950 note), or None when it was taken on another shape or on a
+    library built from other sources than the loaded one."""
     p = os.path.join(REPO, "profiles", f"pmc_{mode}_kernel.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if int(d.get("n_envs", -1)) == n_envs and int(d.get("steps_per_launch", 1)) == steps_per_launch:
+        if (int(d.get("n_envs", -1)) == n_envs and int(d.get("steps_per_launch", 1)) == steps_per_launch
+                and d.get("build_id") == build_id):
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start torch.distributed.run with N ranks of this same
+    command line as a child process (nothing here has touched the GPU) and return its exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def _dp_minibatches(n: int, dev, seed: int):
+    """A rank's synthetic minibatch of n samples: the packed step's six inputs (boards + hand planes,
+    192-way masks with at least one legal action, a legal action, old log-prob, advantage, return)."""
+    import torch
+
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = (torch.rand((n, 4, 8, 8), generator=g) < 0.4).float()
+    masks = (torch.rand((n, 192), generator=g) < 0.3).float()
+    masks[:, 0] = 1.0
+    act = torch.multinomial(masks, 1, generator=g).squeeze(1)
+    lp = -torch.rand(n, generator=g) * 4.0
+    adv = torch.randn(n, generator=g)
+    ret = torch.randn(n, generator=g)
+    return [t.to(dev) for t in (x, masks, act, lp, adv, ret)]
+
+
+def dp_update_leg(dev, rank: int, world: int, steps: int, warmup: int, bf16: bool) -> dict:
+    """Per-rank PPO optimizer steps of 2,048 samples (train_minibatch: HIP-graph-replayed forward, fused loss,
+    backward, gradient all-reduce over the process group -- RCCL on GPUs -- then clip + Adam), timed between
+    barriers (max over ranks), and the same step with no collective (a local agent, world forced to 1): the
+    difference is the all-reduce's exposed time per step.  Plus the full-buffer all-reduce alone."""
+    import torch
+    import torch.distributed as dist
+
+    from agents import ppo as P
+
+    def timed(agent, k, sync_ranks):
+        ins = _dp_minibatches(2048, dev, 1000 + rank)
+        for _ in range(warmup):
+            agent.train_minibatch(*ins)
+        if sync_ranks:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            agent.train_minibatch(*ins)
+        torch.cuda.synchronize(dev)
+        if sync_ranks:
+            dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        if sync_ranks:  # max over ranks (gloo-free: the process group's own device for nccl)
+            el = el.to(dev) if dist.get_backend() == "nccl" else el
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()) / k * 1e3
+
+    def make_agent():
+        torch.manual_seed(0)
+        a = P.PPOAgent(P.PPOConfig(batch_size=2048), device=dev, sample_seed=1)
+        if bf16:
+            a.autocast_dtype = torch.bfloat16
+        a.train()
+        return a
+
+    # the same step without the collective: world forced to 1 for a local agent (its own graphs)
+    P._WORLD_OVERRIDE = 1
+    try:
+        local_ms = timed(make_agent(), steps, sync_ranks=False)
+    finally:
+        P._WORLD_OVERRIDE = None
+    agent = make_agent()
+    P.broadcast_parameters(agent, 0)
+    dp_ms = timed(agent, steps, sync_ranks=True)
+    flat = agent._flat_grad
+    # the full-size collective alone (every gradient float of the model, one buffer)
+    for _ in range(3):
+        dist.all_reduce(flat)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        dist.all_reduce(flat)
+    torch.cuda.synchronize(dev)
+    ar_ms = (time.perf_counter() - t0) / 10 * 1e3
+    # every rank's weights must agree after the data-parallel steps (the all-reduced update is identical)
+    w = torch.cat([p.detach().reshape(-1)[:64].double() for p in agent.network.parameters()])
+    w_max, w_min = w.clone(), w.clone()
+    dist.all_reduce(w_max, op=dist.ReduceOp.MAX)
+    dist.all_reduce(w_min, op=dist.ReduceOp.MIN)
+    return {
+        "workload": ("BASELINE config 5 shape: 131,072 envs per rank's update, bf16 autocast CNN" if bf16 else
+                     "BASELINE config 4 shape: default.yaml PPO, fp32 CNN"),
+        "minibatch_per_rank": 2048, "scope": "per_gpu (training.minibatch_scope)",
+        "dp_overlap": agent.dp_overlap,
+        "backend": dist.get_backend(), "rccl_world_size": dist.get_world_size(),
+        "steps": steps, "warmup": warmup,
+        "step_ms": round(dp_ms, 4), "local_step_ms": round(local_ms, 4),
+        "exposed_allreduce_ms": round(dp_ms - local_ms, 4),
+        "allreduce_alone_ms": round(ar_ms, 4), "grad_floats": int(flat.numel()),
+        "grad_bytes": int(flat.numel() * 4),
+        "allreduce_busbw_gbs": round(2 * (world - 1) / world * flat.numel() * 4 / (ar_ms * 1e-3) / 1e9, 2),
+        "ranks_weights_equal": bool(torch.equal(w_max, w_min)),
+        "samples_per_s": round(world * 2048 / (dp_ms * 1e-3), 1),
+        "optimizer_step": "/root/reference/src/agents/ppo.py:395-401 inside scripts/train.py:173-209",
+    }
 
 
 def main() -> None:
@@ -195,12 +321,24 @@ def main() -> None:
                     help="split the envs into this many handles, one HIP stream each")
     ap.add_argument("--rollout-len", type=int, default=128,
                     help="T, env-steps per bb_rollout launch (default 128 = the reference's PPO horizon n_steps)")
+    ap.add_argument("--dp-steps", type=int, default=20,
+                    help="N > 1: timed optimizer steps per precision in the dp_update leg (0: no leg)")
+    ap.add_argument("--dp-warmup", type=int, default=5)
+    ap.add_argument("--dp-precision", choices=("fp32", "bf16", "both"), default="both",
+                    help="dp_update leg: config 4's fp32 CNN, config 5's bf16 autocast CNN, or both")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: launch N ranks for --gpus N", file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # BB_BENCH_SHARE_GPU=1 (tests only): every rank on cuda:0 over gloo, to
@@ -305,10 +443,20 @@ def main() -> None:
 
     total_env_steps = n * world * args.steps * per_launch
     value = total_env_steps / el
+    for e, _, _, _ in shards:  # the env shards' memory is not needed by the update leg
+        e.close()
+    shards = []
+
+    dp = None
+    if world > 1 and args.dp_steps > 0:
+        dp = {}
+        for prec in (("fp32", "bf16") if args.dp_precision == "both" else (args.dp_precision,)):
+            dp[prec] = dp_update_leg(dev, rank, world, args.dp_steps, args.dp_warmup, prec == "bf16")
     if rank == 0:
         algo_bytes = ALGO_BYTES_PER_ENV_STEP * n * per_launch
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(n, args.mode, per_launch)
+        bid = L.build_id()
+        traffic = load_traffic(n, args.mode, per_launch, bid)
         out = {
             "metric": "env-steps/sec (whole node) at 64k parallel envs, 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -349,19 +497,19 @@ def main() -> None:
                 "kernel_avg_ms": round(kern_ms, 5),
                 "algo_bytes_per_launch": algo_bytes,
             },
-            "build_id": L.build_id(),
+            "build_id": bid,
         }
         if args.mode == "rollout":
             # the binding resource is instruction issue, not bytes: the committed SQ counters
-            out["roofline"]["valu"] = load_valu(n, T)
+            out["roofline"]["valu"] = load_valu(n, T, bid)
+        if dp is not None:
+            out["dp_update"] = dp
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"] = cb
             if not args.no_native_baseline:
                 out["cpu_baseline_native"] = cpu_baseline_native(args.native_seconds)
         print(json.dumps(out), flush=True)
-    for e, _, _, _ in shards:
-        e.close()
     if world > 1:
         dist.destroy_process_group()
 

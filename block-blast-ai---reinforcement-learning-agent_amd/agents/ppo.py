@@ -66,7 +66,13 @@ class PPOConfig:
         return cls(**{k: v for k, v in data.items() if k in cls.__dataclass_fields__})
 
 
+# bench.py's dp_update leg only: a rank's local agent timed without the collective (None: the process group's)
+_WORLD_OVERRIDE: Optional[int] = None
+
+
 def _world() -> int:
+    if _WORLD_OVERRIDE is not None:
+        return _WORLD_OVERRIDE
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
@@ -606,7 +612,7 @@ class PPOAgent(BaseAgent):
             # conv weight gradients beside the rest of the backward (opt-in), or their partial-sum reductions
             # carried by the next BatchNorm backward's launch (every .grad is None here, so autograd keeps the
             # returned tensors and nothing reads them before the block closes)
-            with K.deferred_wgrad(self.device), K.wgrad_piggyback(self.device):
+            with K.deferred_wgrad(self.device), K.wgrad_piggyback(self.device, params=list(self.network.parameters())):
                 self._backward_loss(loss)
         self._clip_and_step()
 
@@ -651,6 +657,15 @@ class PPOAgent(BaseAgent):
                          [opt.state[p]["exp_avg_sq"] for p in params], [opt.state[p]["step"] for p in params],
                          grp["lr"], b1, b2, grp["eps"], self.config.max_grad_norm, ws)
         return True
+
+    def check_optimizer_guard(self) -> None:
+        """Raise when the fused clip + Adam flagged a non-finite or huge gradient-norm operand since the last
+        check (bb_adam_clip_step's guard word, csrc/bb_optim.hip adam_finalize_kernel), naming the parameter."""
+        if not self._adam_ws:
+            return
+        names = [n for n, p in self.network.named_parameters() if p.requires_grad]
+        for key, ws in self._adam_ws.items():
+            K.adam_guard_check(ws, key, names if len(names) == len(key) else None)
 
     def _clip_and_step(self) -> None:
         """clip_grad_norm_(max_grad_norm) + Adam.step() (ppo.py:397-401)."""
@@ -727,9 +742,18 @@ class PPOAgent(BaseAgent):
             opt = {p: {k: v.detach().clone() for k, v in st.items() if torch.is_tensor(v)}
                    for p, st in self.optimizer.state.items()}
         dev_stream = torch.cuda.current_stream(self.device)
+        # the hand-off kernels' counters: a block of this capture's own (zeroed on dev_stream, before the side
+        # stream's fork), kept alive with its graphs
+        own = K.own_counters(self.device).__enter__()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(dev_stream)
         world = _world()
+        try:
+            return self._capture_on(side, dev_stream, world, static_in, params, bufs, rng, rng0, opt, own)
+        finally:
+            own.__exit__(None, None, None)
+
+    def _capture_on(self, side, dev_stream, world, static_in, params, bufs, rng, rng0, opt, own):
         with torch.cuda.stream(side):
             for _ in range(3):
                 loss, _ = self._minibatch_loss(*static_in)
@@ -797,6 +821,7 @@ class PPOAgent(BaseAgent):
                             v.copy_(old[k])
                         else:  # fresh Adam state == zero moments at step 0
                             v.zero_()
+        graphs[0].bb_counters = own.block  # the graphs embed its address
         return graphs, static_in, stats, flat
 
     def update(self, buffer, last_values, batch_size: Optional[int] = None) -> Dict[str, float]:
@@ -829,6 +854,7 @@ class PPOAgent(BaseAgent):
                     self.minibatch_callback(n, st)
                 n += 1
         m = (acc / max(n, 1)).tolist()
+        self.check_optimizer_guard()
         keys = ("policy_loss", "value_loss", "entropy", "total_loss", "approx_kl", "clip_fraction")
         return dict(zip(keys, m))
 

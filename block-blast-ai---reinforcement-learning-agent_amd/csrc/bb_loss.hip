@@ -124,9 +124,10 @@ __device__ __forceinline__ void row_forward(const void* __restrict__ logits, con
   r.ent = -wsum(h);
 }
 
-// Write-through hand-off of the blocks' partial sums (MI355X_MICROARCH.md, fence-free form): stored sc1 by the
-// storing wave, drained, then one lane counts the block; the block whose add returns the last count reads all
-// partials sc1 and finalises.
+// Last-arriver hand-off of the blocks' partial sums, ordered by the HIP memory model: stored by agent-scope atomic
+// stores (written through, sc1) and drained, a workgroup barrier, then one lane counts the block with an agent-scope
+// acq_rel add (release: buffer_wbl2 sc1 + s_waitcnt before it; acquire: buffer_inv sc1 after it); the block whose add
+// returns the last count reads all partials with agent-scope loads, finalises and re-arms the counter atomically.
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) uint32_t guint32;
 __device__ __forceinline__ void wt_store(double* p, double v) {
@@ -136,7 +137,7 @@ __device__ __forceinline__ double wt_load(const double* p) {
   return __hip_atomic_load((const gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t wt_arrive(uint32_t* c) {
-  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -264,7 +265,7 @@ __global__ void __launch_bounds__(kLossThreads) ppo_loss_kernel(
       for (int l = 0; l < 64; ++l) t[k] += lsum[k][l];
     }
     loss_stats_out(t, B, vcoef, ecoef, stats, loss);
-    cnt[0] = 0u;  // every block has counted itself: re-armed for the next launch
+    __hip_atomic_store((guint32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
   }
 }
 

@@ -154,24 +154,62 @@ __global__ void __launch_bounds__(kOptThreads) adam_norm_kernel(const AdamTable 
   }
 }
 
+// Guard on the norm's inputs: a chunk partial (the sum of g^2 over 2,048 elements) that is not finite or above
+// kGuardChunkSq (a chunk L2 norm above 1e8, ~1e5x the largest this network's gradients reach) is an operand that
+// no gradient kernel should have produced -- e.g. a read of an unwritten workspace.  The finaliser records the
+// first such chunk in header word kGuardWord as chunk + 1 (sticky: only the first offence is kept until the host
+// clears it) and counts offences in kGuardWord + 1; the update itself is not altered (clip_grad_norm_'s
+// arithmetic on whatever the gradients hold).  PPOAgent.update reads the word once per update and raises.
+constexpr double kGuardChunkSq = 1e16;
+constexpr int kGuardWord = 2;  // uint32 words 2, 3 of the header (floats 2..15 are unused)
+
 __global__ void __launch_bounds__(kOptThreads) adam_finalize_kernel(const AdamTable tab, double* __restrict__ ws,
                                                                     float max_norm, double beta1, double beta2,
                                                                     float* __restrict__ norm_out) {
   __shared__ double red[kOptThreads / 64];
+  __shared__ uint32_t bad_first, bad_count;
+  if (threadIdx.x == 0) {
+    bad_first = 0xffffffffu;
+    bad_count = 0u;
+  }
+  __syncthreads();
   const int nchunks = tab.chunk0[tab.count];
   double s = 0.0;
+  uint32_t my_first = 0xffffffffu, my_count = 0u;
+  auto guard = [&](double v, int c) {
+    if (!(v <= kGuardChunkSq)) {  // NaN fails the comparison too
+      my_first = min(my_first, (uint32_t)c);
+      ++my_count;
+    }
+  };
   int i = threadIdx.x;
   for (; i + 7 * kOptThreads < nchunks; i += 8 * kOptThreads) {  // 8 loads in flight, added in order
     double v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = ws[kHdr + i + j * kOptThreads];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += v[j];
+    for (int j = 0; j < 8; ++j) {
+      s += v[j];
+      guard(v[j], i + j * kOptThreads);
+    }
   }
-  for (; i < nchunks; i += kOptThreads) s += ws[kHdr + i];
-  s = block_sum(s, red);
+  for (; i < nchunks; i += kOptThreads) {
+    const double v = ws[kHdr + i];
+    s += v;
+    guard(v, i);
+  }
+  if (my_count) {
+    atomicMin(&bad_first, my_first);
+    atomicAdd(&bad_count, my_count);
+  }
+  s = block_sum(s, red);  // (its barrier orders the LDS atomics above before thread 0's reads below)
   float* hdr = reinterpret_cast<float*>(ws);
   if (threadIdx.x == 0) {
+    uint32_t* gw = reinterpret_cast<uint32_t*>(ws) + kGuardWord;
+    if (bad_count) {
+      if (gw[0] == 0u) gw[0] = bad_first + 1u;
+      gw[1] += bad_count;
+    }
     // clip_grad_norm_: total_norm (f32), clip_coef = max_norm / (total_norm + 1e-6), clamped to <= 1
     const float norm = float(sqrt(s));
     const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);
@@ -343,10 +381,12 @@ constexpr int kBgradCols = 8 * kBgradCL;
 constexpr int kBgradChunk = BB_BGRAD_CFG == 0 ? BB_BGRAD_CHUNK : BB_BGRAD_CFG == 3 ? 512 : 0;  // rows per chunk
 constexpr int kBgradMaxSplit = 64;
 
-// Write-through hand-off (MI355X_MICROARCH.md, fence-free form): partial sums stored with agent-scope relaxed
-// atomic stores (sc1, written through to L2), the storing wave drains them (s_waitcnt vmcnt(0)), a barrier,
-// then one lane counts the workgroup on an agent-scope counter; the workgroup whose add returns the last count
-// reads every partial with agent-scope loads.
+// Last-arriver hand-off between workgroups, ordered by the HIP memory model rather than by hardware behaviour:
+// partial sums stored with agent-scope atomic stores (written through, sc1), a workgroup barrier (every wave's
+// stores issued before the count), then one lane counts the workgroup with an agent-scope acq_rel add -- its
+// release half (buffer_wbl2 sc1 + s_waitcnt vmcnt(0) before the add) publishes the partials of every wave
+// that passed the barrier, its acquire half (buffer_inv sc1 after it) keeps the last arriver's loads from
+// seeing anything older.  The re-arm of the counter is an agent-scope atomic store.
 typedef __attribute__((address_space(1))) float gfloat;
 typedef __attribute__((address_space(1))) uint32_t guint32;
 __device__ __forceinline__ void wt_store(float* p, float v) {
@@ -356,8 +396,13 @@ __device__ __forceinline__ float wt_load(const float* p) {
   return __hip_atomic_load((const gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t wt_arrive(uint32_t* c) {
-  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void wt_rearm(uint32_t* c) {
+  __hip_atomic_store((guint32*)c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the waves' own stores complete before the barrier that precedes the arrive (the release covers them too;
+// kept so a wave never reaches the barrier with its partial stores still in flight)
 __device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 struct Philox4 {
@@ -530,7 +575,7 @@ __global__ void __launch_bounds__(kBgradThreads) linear_bgrad_kernel(const uint1
 #pragma unroll
   for (int k = 0; k < kBgradMaxSplit; ++k) t += v[k];  // chunk order; absent chunks add +0
   if (c < cols) db[c] = f2bf_rne(t);
-  if (threadIdx.x == 0) cnt[blockIdx.x] = 0u;  // every chunk has counted itself: re-armed for the next launch
+  if (threadIdx.x == 0) wt_rearm(cnt + blockIdx.x);  // every chunk has counted itself: re-armed for the next launch
 }
 
 // Weight gradient of a bf16 Linear, dW[n][k] = sum_r g[r][n] x[r][k] (autograd's g^T x for the CNN's small
@@ -643,7 +688,7 @@ __global__ void __launch_bounds__(256) linear_wgrad_kernel(const uint16_t* __res
       }
       v[u] = sum;
     }
-    if (t == 0) cnt[tile] = 0u;  // every split has counted itself: re-armed for the next launch
+    if (t == 0) wt_rearm(cnt + tile);  // every split has counted itself: re-armed for the next launch
   }
 #pragma unroll
   for (int u = 0; u < kOut; ++u) {
@@ -759,7 +804,7 @@ __global__ void __launch_bounds__(256) linear_n1_bwd_kernel(const uint16_t* __re
       }
       v = sum;
     }
-    if (t == 0) cnt[blockIdx.x] = 0u;
+    if (t == 0) wt_rearm(cnt + blockIdx.x);
   }
   if (t < kBgradCols) {
     const int c = blockIdx.x * kBgradCols + t;

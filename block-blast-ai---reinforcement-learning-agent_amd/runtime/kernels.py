@@ -6,6 +6,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import struct
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -370,7 +371,7 @@ _wg_active = {}  # device -> [depth, used]
 
 class deferred_wgrad:
     def __init__(self, device: torch.device, enabled: bool = True):
-        self.dev = torch.device(device)
+        self.dev = _dev_key(device)
         self.on = bool(enabled and ASYNC_WGRAD and self.dev.type == "cuda")
 
     def __enter__(self):
@@ -393,6 +394,7 @@ def _wgrad_deferred(weight: torch.Tensor, dev: torch.device, saved, compute) -> 
     """Run compute() -> dw on the side stream and add it into weight.grad there when a deferred_wgrad block
     is open on ``dev``; False (nothing done) otherwise.  ``saved``: tensors of the current stream that the
     side stream reads (kept from reuse until it has)."""
+    dev = _dev_key(dev)
     st = _wg_active.get(dev)
     if not st or st[0] <= 0 or weight.grad is not None and weight.grad.is_sparse:
         return False
@@ -439,7 +441,7 @@ def _flush_reduce(dev, job) -> None:
 
 
 def _take_pending_reduce(dev):
-    st = _pending_red.get(torch.device(dev))
+    st = _pending_red.get(_dev_key(dev))
     if not st or st[1] is None:
         return None
     job, st[1] = st[1], None
@@ -447,12 +449,18 @@ def _take_pending_reduce(dev):
 
 
 class wgrad_piggyback:
-    def __init__(self, device: torch.device, enabled: bool = True):
-        self.dev = torch.device(device)
+    """``params``: the parameters whose gradients the backward inside produces; every .grad must be None at
+    entry (autograd then keeps the tensors the reductions write instead of adding them into old ones)."""
+
+    def __init__(self, device: torch.device, enabled: bool = True, params=None):
+        self.dev = _dev_key(device)
         self.on = bool(enabled and WGRAD_PIGGYBACK and self.dev.type == "cuda")
+        self.params = params
 
     def __enter__(self):
         if self.on:
+            if self.params is not None and any(p.grad is not None for p in self.params):
+                raise L.BBNativeError("wgrad_piggyback: every parameter's .grad must be None when the block opens")
             _pending_red.setdefault(self.dev, [0, None, []])[0] += 1
         return self
 
@@ -619,8 +627,8 @@ class Conv3x3Function(torch.autograd.Function):
                         "bb_conv3x3_wgrad")
                 return g
 
-            st = _pending_red.get(torch.device(dev))
-            if st and st[0] > 0 and not _wg_active.get(dev, [0])[0] > 0:
+            st = _pending_red.get(_dev_key(dev))
+            if st and st[0] > 0 and not _wg_active.get(_dev_key(dev), [0])[0] > 0:
                 # partial sums now, their reduction in the next BatchNorm backward's finalisation launch
                 prev = _take_pending_reduce(dev)
                 if prev is not None:
@@ -842,11 +850,41 @@ def _ptrs(ts):
 
 
 def adam_clip_workspace(numels, device) -> torch.Tensor:
+    """bb_adam_clip_step's scratch, zeroed: its header holds the guard word (ADAM_GUARD_WORD) the finaliser
+    sets and adam_guard_check reads."""
     n = (C.c_int64 * len(numels))(*numels)
     nbytes = L.load().bb_adam_clip_workspace_bytes(len(numels), n)
     if nbytes < 0:
         raise L.BBNativeError(f"bb_adam_clip_workspace_bytes rejected {len(numels)} tensors")
-    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+    return torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=device)
+
+
+ADAM_GUARD_WORD = 2  # BB_ADAM_GUARD_WORD: uint32 words 2 (first bad chunk + 1) and 3 (count) of the header
+ADAM_CHUNK = 2048  # elements per gradient-norm chunk
+
+
+def adam_guard_check(ws: torch.Tensor, numels, names=None, clear: bool = True) -> None:
+    """Raise BBNativeError when bb_adam_clip_step's finaliser flagged a gradient-norm chunk partial that was
+    not finite or above 1e16 (sum of g^2 over 2,048 elements), naming the tensor and the element range.  One
+    device read (a sync); ``clear`` re-arms the word."""
+    w = ws.view(torch.int32)[ADAM_GUARD_WORD:ADAM_GUARD_WORD + 2]
+    first, count = (int(v) for v in w.tolist())
+    if first == 0:
+        return
+    if clear:
+        w.zero_()
+    chunk = first - 1
+    t, c0 = 0, 0
+    for t, n in enumerate(numels):
+        nc = -(-int(n) // ADAM_CHUNK)
+        if chunk < c0 + nc:
+            break
+        c0 += nc
+    lo = (chunk - c0) * ADAM_CHUNK
+    name = names[t] if names is not None and t < len(names) else f"tensor {t}"
+    raise L.BBNativeError(f"bb_adam_clip_step guard: {count} gradient-norm chunk partial(s) non-finite or above "
+                          f"1e16; first: {name} elements [{lo}, {min(lo + ADAM_CHUNK, int(numels[t]))}) "
+                          f"(chunk {chunk})")
 
 
 def adam_clip_step(params, grads, exp_avgs, exp_avg_sqs, steps, lr: float, beta1: float, beta2: float, eps: float,
@@ -899,20 +937,68 @@ def _rows_ok(t: torch.Tensor) -> bool:
 
 _bgrad_cnt = {}  # (device, stream) -> zeroed uint32 counters of bb_linear_bgrad (re-armed by every launch)
 _BGRAD_CNT = 4096
+_cnt_owned = {}  # device key -> the counter block of the capture in progress (own_counters)
+_cnt_live = weakref.WeakValueDictionary()  # id -> every capture-owned block still referenced (by its graph)
+
+
+def _dev_key(dev) -> torch.device:
+    """A device with its index ('cuda' -> 'cuda:<current>'), the key every per-device table here uses."""
+    d = torch.device(dev)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+class own_counters:
+    """A counter block of its own for the launches issued inside (a graph capture and its warm-up): the
+    hand-off kernels of a captured graph embed its address, so two graphs never share counters through a
+    pooled stream handle.  ``block`` is the tensor; keep it alive as long as the graph (PPOAgent stores it with
+    the captured entry).  Created zeroed, before any capture starts."""
+
+    def __init__(self, device):
+        self.dev = _dev_key(device)
+        self.block = None
+        self._prev = None
+
+    def __enter__(self):
+        if self.dev.type == "cuda":
+            self.block = torch.zeros(_BGRAD_CNT, dtype=torch.int32, device=self.dev)
+            _cnt_live[id(self.block)] = self.block
+            self._prev = _cnt_owned.get(self.dev)
+            _cnt_owned[self.dev] = self.block
+        return self
+
+    def __exit__(self, *exc):
+        if self.dev.type == "cuda":
+            if self._prev is None:
+                _cnt_owned.pop(self.dev, None)
+            else:
+                _cnt_owned[self.dev] = self._prev
+        return False
+
+
+def counter_blocks():
+    """Every counter block handed out so far (stream-keyed and capture-owned ones alike are re-armed by the
+    launches that used them: all zero between steps -- tests check it)."""
+    return list(_bgrad_cnt.values()) + list(_cnt_live.values())
 
 
 def _bgrad_counters(dev: torch.device, need: int) -> torch.Tensor:
-    """The stream's zeroed counter block (bb_linear_bgrad / bb_linear_wgrad; launches on one stream are
-    ordered, and each re-arms the counters it used)."""
+    """The zeroed counter block for a hand-off launch: the capture's own (own_counters) when one is open on
+    the device, else the stream's (launches on one stream are ordered, and each re-arms the counters it used)."""
     if need > _BGRAD_CNT:
         raise L.BBNativeError(f"linear tails: {need} counters needed (> {_BGRAD_CNT})")
-    stream = torch.cuda.current_stream(dev)
-    key = (str(dev), stream.cuda_stream)
+    dk = _dev_key(dev)
+    own = _cnt_owned.get(dk)
+    if own is not None:
+        return own
+    stream = torch.cuda.current_stream(dk)
+    key = (str(dk), stream.cuda_stream)
     cnt = _bgrad_cnt.get(key)
     if cnt is None:
         if torch.cuda.is_current_stream_capturing():  # zeroed outside capture: a captured fill would re-zero
             raise L.BBNativeError("linear_bgrad: run one eager backward on this stream before capturing")
-        cnt = _bgrad_cnt[key] = torch.zeros(_BGRAD_CNT, dtype=torch.int32, device=dev)
+        cnt = _bgrad_cnt[key] = torch.zeros(_BGRAD_CNT, dtype=torch.int32, device=dk)
     return cnt
 
 

@@ -125,11 +125,33 @@ def test_bench_two_ranks_shared_gpu(tmp_path):
     env = dict(os.environ, BB_BENCH_SHARE_GPU="1", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={29900 + os.getpid() % 50}",
-           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "10", "--warmup", "3", "--envs", "4096"]
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "10", "--warmup", "3", "--envs", "4096",
+           "--dp-steps", "0"]
     r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1  # rank 0 only
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_envs"] == 8192 and d["value"] > 0
-    assert d["scaling"] == "weak" and "cpu_baseline" not in d
+    assert d["scaling"] == "weak" and "cpu_baseline" not in d and "dp_update" not in d
+
+
+def test_bench_gpus_flag_launches_ranks(tmp_path):
+    """`python bench.py --gpus 2` with no launcher starts its own two ranks (the driver's plain form) and adds
+    the dp_update leg: per-rank optimizer steps with the gradient all-reduce, both precisions (share mode:
+    both ranks on cuda:0 over gloo -- the RCCL world is the driver's 8-GPU run)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BB_BENCH_SHARE_GPU"] = "1"
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
+           "--envs", "4096", "--dp-steps", "3", "--dp-warmup", "1"]
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_envs"] == 8192
+    for prec in ("fp32", "bf16"):
+        dp = d["dp_update"][prec]
+        assert dp["rccl_world_size"] == 2 and dp["step_ms"] > 0 and dp["local_step_ms"] > 0
+        assert dp["ranks_weights_equal"], dp  # the all-reduced updates left both ranks on the same weights
+        assert dp["grad_floats"] >= 5_290_113

@@ -91,6 +91,61 @@ def test_adam_clip_rejects_bad_tables(cuda):
     assert L.load().bb_adam_clip_workspace_bytes(0, None) < 0
 
 
+@pytest.mark.parametrize("bad", [float("nan"), 3e9])
+def test_adam_clip_guard_names_the_chunk(cuda, bad):
+    """A non-finite or huge gradient-norm operand (the round-5 one-off: a clip norm ~1e10x too large) is
+    flagged on the device and raised by the host check with the tensor and element range; a clean step after
+    the check leaves the word clear."""
+    from runtime import kernels as K
+    from runtime import lib as L
+
+    ps = _tensors(cuda, 3)
+    gs = _tensors(cuda, 4)
+    m = [torch.zeros_like(p) for p in ps]
+    v = [torch.zeros_like(p) for p in ps]
+    steps = [torch.zeros((), device=cuda) for _ in ps]
+    numels = [p.numel() for p in ps]
+    names = [f"p{i}" for i in range(len(ps))]
+    ws = K.adam_clip_workspace(numels, cuda)
+    K.adam_clip_step(ps, gs, m, v, steps, 1e-3, 0.9, 0.999, 1e-5, 0.5, ws)
+    K.adam_guard_check(ws, numels, names)  # clean
+    gs[0].view(-1)[5000] = bad  # (512, 8192): its chunk 2 holds element 5000
+    K.adam_clip_step(ps, gs, m, v, steps, 1e-3, 0.9, 0.999, 1e-5, 0.5, ws)
+    with pytest.raises(L.BBNativeError, match=r"p0 elements \[4096, 6144\)"):
+        K.adam_guard_check(ws, numels, names)
+    gs = _tensors(cuda, 5)
+    K.adam_clip_step(ps, gs, m, v, steps, 1e-3, 0.9, 0.999, 1e-5, 0.5, ws)
+    K.adam_guard_check(ws, numels, names)  # cleared by the check
+
+
+def test_counters_rearmed_after_update(cuda):
+    """Every hand-off counter block (stream-keyed and capture-owned) is back to zero after bf16 and fp32
+    graph-replayed optimizer steps: no launch left a counter armed."""
+    from agents import PPOAgent, PPOConfig
+    from runtime import kernels as K
+
+    for bf16 in (False, True):
+        torch.manual_seed(0)
+        agent = PPOAgent(PPOConfig(batch_size=256), device=cuda, sample_seed=1)
+        if bf16:
+            agent.autocast_dtype = torch.bfloat16
+        agent.train()
+        g = torch.Generator().manual_seed(1)
+        x = (torch.rand((256, 4, 8, 8), generator=g) < 0.4).float().to(cuda)
+        masks = (torch.rand((256, 192), generator=g) < 0.3).float()
+        masks[:, 0] = 1.0
+        act = torch.multinomial(masks, 1, generator=g).squeeze(1).to(cuda)
+        ins = (x, masks.to(cuda), act, -torch.rand(256).to(cuda), torch.randn(256).to(cuda), torch.randn(256).to(cuda))
+        for _ in range(5):
+            agent.train_minibatch(*ins)
+        torch.cuda.synchronize()
+        blocks = K.counter_blocks()
+        assert blocks and all(int(b.abs().sum()) == 0 for b in blocks)
+        agent.check_optimizer_guard()
+        ent = next(iter(agent._graphs.values()))
+        assert getattr(ent[0][0], "bb_counters", None) is not None  # the capture's own block, kept with it
+
+
 def test_cast_multi_exact(cuda):
     from runtime import kernels as K
 

@@ -55,6 +55,14 @@ def main():
     out = {"n_envs": a.envs, "steps_per_launch": a.steps_per_launch, "hbm_bytes_per_launch": round(total),
            "per_kernel": per, "bytes_per_env_step": round(total / a.envs / a.steps_per_launch, 2),
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; FETCH_SIZE x2 (gfx950)"}
+    try:  # the sources the profiled library was built from (runtime.lib.load() refuses any other)
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "block-blast-ai---reinforcement-learning-agent_amd"))
+        from runtime.build import source_id
+        out["build_id"] = source_id()
+    except Exception:  # noqa: BLE001
+        pass
     s = json.dumps(out, indent=1)
     print(s)
     if a.out:
