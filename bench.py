@@ -326,6 +326,8 @@ def main() -> None:
     ap.add_argument("--dp-warmup", type=int, default=5)
     ap.add_argument("--dp-precision", choices=("fp32", "bf16", "both"), default="both",
                     help="dp_update leg: config 4's fp32 CNN, config 5's bf16 autocast CNN, or both")
+    ap.add_argument("--dp-timeout", type=float, default=300.0,
+                    help="dp_update leg watchdog (s): on expiry rank 0 prints the line with the error")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -447,12 +449,8 @@ def main() -> None:
         e.close()
     shards = []
 
-    dp = None
-    if world > 1 and args.dp_steps > 0:
-        dp = {}
-        for prec in (("fp32", "bf16") if args.dp_precision == "both" else (args.dp_precision,)):
-            dp[prec] = dp_update_leg(dev, rank, world, args.dp_steps, args.dp_warmup, prec == "bf16")
-    if rank == 0:
+    def line(dp_block):
+        """The bench line (rank 0 prints it)."""
         algo_bytes = ALGO_BYTES_PER_ENV_STEP * n * per_launch
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         bid = L.build_id()
@@ -502,8 +500,38 @@ def main() -> None:
         if args.mode == "rollout":
             # the binding resource is instruction issue, not bytes: the committed SQ counters
             out["roofline"]["valu"] = load_valu(n, T, bid)
-        if dp is not None:
-            out["dp_update"] = dp
+        if dp_block is not None:
+            out["dp_update"] = dp_block
+        return out
+
+    dp = None
+    if world > 1 and args.dp_steps > 0:
+        # the env line is already measured: a dp_update leg that fails or hangs (a collective that never
+        # completes) must not cost it.  A watchdog per rank prints rank 0's line with the error and ends
+        # every rank with status 0 after --dp-timeout seconds; an exception is recorded likewise.
+        import threading
+
+        dp = {}
+
+        def expire():
+            if rank == 0:
+                dp["error"] = f"dp_update leg timed out after {args.dp_timeout:.0f} s"
+                print(json.dumps(line(dp)), flush=True)
+            print(f"[bench] rank {rank}: dp_update watchdog fired", file=sys.stderr, flush=True)
+            os._exit(0)
+
+        dog = threading.Timer(args.dp_timeout, expire)
+        dog.daemon = True
+        dog.start()
+        try:
+            for prec in (("fp32", "bf16") if args.dp_precision == "both" else (args.dp_precision,)):
+                dp[prec] = dp_update_leg(dev, rank, world, args.dp_steps, args.dp_warmup, prec == "bf16")
+        except Exception as exc:  # noqa: BLE001 -- reported in the line, never lost
+            dp["error"] = f"{type(exc).__name__}: {exc}"[:500]
+            print(f"[bench] rank {rank}: dp_update leg failed: {dp['error']}", file=sys.stderr, flush=True)
+        dog.cancel()
+    if rank == 0:
+        out = line(dp)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(args.cpu_seconds)
             out["cpu_baseline"] = cb

@@ -124,10 +124,14 @@ __device__ __forceinline__ void row_forward(const void* __restrict__ logits, con
   r.ent = -wsum(h);
 }
 
-// Last-arriver hand-off of the blocks' partial sums, ordered by the HIP memory model: stored by agent-scope atomic
-// stores (written through, sc1) and drained, a workgroup barrier, then one lane counts the block with an agent-scope
-// acq_rel add (release: buffer_wbl2 sc1 + s_waitcnt before it; acquire: buffer_inv sc1 after it); the block whose add
-// returns the last count reads all partials with agent-scope loads, finalises and re-arms the counter atomically.
+// Last-arriver hand-off of the blocks' partial sums, ordered by the HIP memory model (as bb_optim.hip's): stored by
+// agent-scope atomic stores (written through, sc1) and drained, a workgroup barrier, then one lane counts the block
+// with an agent-scope release add (buffer_wbl2 sc1 + s_waitcnt before it); the lane whose add returns the last count
+// issues an agent-scope acquire fence (buffer_inv sc1) and its block, after a barrier, reads all partials with
+// agent-scope loads, finalises and re-arms the counter atomically.
+#ifndef BB_HANDOFF_ORDER
+#define BB_HANDOFF_ORDER __ATOMIC_RELEASE  // A/B only: __ATOMIC_RELAXED is the round-5 form (tools/variants.py hrx)
+#endif
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) uint32_t guint32;
 __device__ __forceinline__ void wt_store(double* p, double v) {
@@ -136,8 +140,10 @@ __device__ __forceinline__ void wt_store(double* p, double v) {
 __device__ __forceinline__ double wt_load(const double* p) {
   return __hip_atomic_load((const gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t wt_arrive(uint32_t* c) {
-  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ bool wt_arrive_last(uint32_t* c, uint32_t n) {
+  const bool last = __hip_atomic_fetch_add((guint32*)c, 1u, BB_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) == n - 1u;
+  if (last && BB_HANDOFF_ORDER != __ATOMIC_RELAXED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return last;
 }
 __device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -239,7 +245,7 @@ __global__ void __launch_bounds__(kLossThreads) ppo_loss_kernel(
     wt_drain();
   }
   __syncthreads();  // wave 0's partial stores have drained
-  if (threadIdx.x == 0) last_block = wt_arrive(cnt) == (uint32_t)(gridDim.x - 1);
+  if (threadIdx.x == 0) last_block = wt_arrive_last(cnt, (uint32_t)gridDim.x);
   __syncthreads();
   if (!last_block) return;
   // every block's partials: lane l of wave k adds blocks (l + 64 j) for stat k (waves 0-3 take stats 0-3, wave 0

@@ -383,10 +383,15 @@ constexpr int kBgradMaxSplit = 64;
 
 // Last-arriver hand-off between workgroups, ordered by the HIP memory model rather than by hardware behaviour:
 // partial sums stored with agent-scope atomic stores (written through, sc1), a workgroup barrier (every wave's
-// stores issued before the count), then one lane counts the workgroup with an agent-scope acq_rel add -- its
-// release half (buffer_wbl2 sc1 + s_waitcnt vmcnt(0) before the add) publishes the partials of every wave
-// that passed the barrier, its acquire half (buffer_inv sc1 after it) keeps the last arriver's loads from
-// seeing anything older.  The re-arm of the counter is an agent-scope atomic store.
+// stores issued before the count), then one lane counts the workgroup with an agent-scope release add
+// (buffer_wbl2 sc1 + s_waitcnt vmcnt(0) before it: the partials of every wave that passed the barrier are
+// published); the lane whose add returns the last count issues an agent-scope acquire fence (buffer_inv sc1)
+// before its workgroup -- after a barrier, or in the same wave -- loads the partials.  The other workgroups skip
+// the acquire (acq_rel on every add: 1.510 against 1.478 ms per bf16 step, profiles/r06/handoff/).  The re-arm
+// of the counter is an agent-scope atomic store.
+#ifndef BB_HANDOFF_ORDER
+#define BB_HANDOFF_ORDER __ATOMIC_RELEASE  // A/B only: __ATOMIC_RELAXED is the round-5 form (tools/variants.py hrx)
+#endif
 typedef __attribute__((address_space(1))) float gfloat;
 typedef __attribute__((address_space(1))) uint32_t guint32;
 __device__ __forceinline__ void wt_store(float* p, float v) {
@@ -395,8 +400,11 @@ __device__ __forceinline__ void wt_store(float* p, float v) {
 __device__ __forceinline__ float wt_load(const float* p) {
   return __hip_atomic_load((const gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t wt_arrive(uint32_t* c) {
-  return __hip_atomic_fetch_add((guint32*)c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+// true in the lane whose add completes the count n (it has then acquired every other workgroup's release)
+__device__ __forceinline__ bool wt_arrive_last(uint32_t* c, uint32_t n) {
+  const bool last = __hip_atomic_fetch_add((guint32*)c, 1u, BB_HANDOFF_ORDER, __HIP_MEMORY_SCOPE_AGENT) == n - 1u;
+  if (last && BB_HANDOFF_ORDER != __ATOMIC_RELAXED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return last;
 }
 __device__ __forceinline__ void wt_rearm(uint32_t* c) {
   __hip_atomic_store((guint32*)c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -566,7 +574,7 @@ __global__ void __launch_bounds__(kBgradThreads) linear_bgrad_kernel(const uint1
   wt_store(col + (size_t)blockIdx.y * kBgradCols, s);
   wt_drain();
   int arrived = 0;
-  if (threadIdx.x == 0) arrived = wt_arrive(cnt + blockIdx.x) == (uint32_t)(nsplit - 1);
+  if (threadIdx.x == 0) arrived = wt_arrive_last(cnt + blockIdx.x, (uint32_t)nsplit);
   if (!__shfl(arrived, 0, 64)) return;  // lane 0's add has returned
   float v[kBgradMaxSplit];
 #pragma unroll
@@ -672,7 +680,7 @@ __global__ void __launch_bounds__(256) linear_wgrad_kernel(const uint16_t* __res
     for (int u = 0; u < kOut; ++u) wt_store(tp + (size_t)blockIdx.z * (kWgT * kWgT) + t + 256 * u, v[u]);
     wt_drain();
     __syncthreads();  // every wave's partial stores have drained
-    if (t == 0) last_split = wt_arrive(cnt + tile) == (uint32_t)(nsplit - 1);
+    if (t == 0) last_split = wt_arrive_last(cnt + tile, (uint32_t)nsplit);
     __syncthreads();
     if (!last_split) return;
 #pragma unroll
@@ -790,7 +798,7 @@ __global__ void __launch_bounds__(256) linear_n1_bwd_kernel(const uint16_t* __re
     if (t < kN1Slots) wt_store(col + (size_t)blockIdx.y * kN1Slots, v);
     wt_drain();
     __syncthreads();  // the storing waves have drained
-    if (t == 0) last_chunk = wt_arrive(cnt + blockIdx.x) == (uint32_t)(nsplit - 1);
+    if (t == 0) last_chunk = wt_arrive_last(cnt + blockIdx.x, (uint32_t)nsplit);
     __syncthreads();
     if (!last_chunk) return;
     if (t < kN1Slots) {

@@ -27,6 +27,8 @@ VARIANTS = {
     "fin4": ["-DBB_BN_FIN_CPB=4"],
     # the gradient-norm pass: four 2,048-element chunks per workgroup (measured slower)
     "an4": ["-DBB_ADAM_NORM_CPB=4"],
+    # round 6: the last-arriver hand-offs' arrive add relaxed (the round-5 form) instead of acq_rel
+    "hrx": ["-DBB_HANDOFF_ORDER=__ATOMIC_RELAXED"],
     # round 5: search waves' pass schedule -- 0: gen_hands_multi's packed passes (round 4); quota per attempt
     # in a round's first pass (shipped 4) and later passes (shipped 64)
     "mq0": ["-DBB_SEARCH_QUOTA=0"],
