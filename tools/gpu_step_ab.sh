@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-sab}; R=$GRAFT_REPO_ROOT
-libof() { [ "$1" = main ] && echo "$R/block-blast-ai---reinforcement-learning-agent_amd/libbbvec.so" || echo "$R/tools/variants/libbbvec_$1.so"; }
+libof() { [ "$1" = main ] && echo "$R/block-blast-ai---reinforcement-learning-agent_amd/libbbvec.so" || echo "$R/build/ab/libbbvec_$1.so"; }
 for v in ${VARIANTS:-main}; do
   BBVEC_LIB=$(libof $v) timeout -k 10 600 python -u -m pytest tests/test_gpu_env_parity.py tests/test_gpu_solver_stress.py \
     tests/test_gpu_full_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
