@@ -501,8 +501,16 @@ int bb_linear_f32(const float* d_x, const float* d_w, const float* d_bias, int32
  * caller scratch of bb_adam_clip_workspace_bytes(num_tensors, h_numel) bytes
  * (16-byte aligned).  Three kernel launches on `stream`; the tensor table is
  * passed by value, so the launches can be captured into a HIP graph.  The norm
- * is summed in a fixed order: deterministic. */
+ * is summed in a fixed order: deterministic.
+ * Guard: zero d_ws once before the first call.  Then uint32 word
+ * BB_ADAM_GUARD_WORD of d_ws holds 1 + the first chunk (BB_ADAM_CHUNK gradient
+ * elements, chunks numbered across the tensors in table order) whose sum of
+ * squares was non-finite or above 1e16.  The next word counts such chunks.
+ * Both are sticky until the caller clears them.  The update itself is not
+ * altered (runtime/kernels.py adam_guard_check reads and clears them). */
 #define BB_OPT_MAX_TENSORS 48
+#define BB_ADAM_GUARD_WORD 2
+#define BB_ADAM_CHUNK 2048
 int64_t bb_adam_clip_workspace_bytes(int32_t num_tensors, const int64_t* h_numel);
 int bb_adam_clip_step(int32_t num_tensors, float* const* h_param, float* const* h_grad,
                       float* const* h_exp_avg, float* const* h_exp_avg_sq, float* const* h_step,

@@ -70,6 +70,13 @@ def main():
             "cyc_per_call": round(ws[:, 2].sum() / max(ws[:, 0].sum(), 1), 0),
             "search_busy_frac": round(ws[:, 2].sum() / (we[:, 1].mean() * len(ws)), 3),
             "polls_per_wave": round(ws[:, 3].mean(), 1),
+            # by env-wave index inside the workgroup (wave k's records are claimed k-th by the search lanes):
+            # mean cycles, and how often that index is its workgroup's slowest env wave
+            "env_wave_cyc_by_index": [round(float(we[k::ew, 1].mean()), 0) for k in range(ew)],
+            "slowest_index_share": [round(float(v), 3) for v in np.bincount(
+                we[:, 1].reshape(-1, ew).argmax(axis=1), minlength=ew) / max(len(we) // ew, 1)],
+            "wg_cyc_max_over_mean": round(float(we[:, 1].reshape(-1, ew).max(axis=1).max() / we[:, 1].mean()), 4),
+            "wg_cyc_mean_of_max": round(float(we[:, 1].reshape(-1, ew).max(axis=1).mean()), 0),
             "call_phase_cyc": {k: round(float(v), 0) for k, v in zip(
                 ("setup_draws", "anchors_pack", "pass_quick", "pass_exact", "pass_overhead", "resolve"), ph)},
         })

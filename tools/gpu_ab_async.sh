@@ -10,7 +10,7 @@ mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-ab}; R=$GRAFT_REPO_ROOT
 # a variant is a library name (tools/variants.py; "main" = the shipped build), optionally followed by
 # runtime settings: "main:BB_PACK_FIRST=4:BB_PACK_NEXT=16"
-libof() { local n=${1%%:*}; [ "$n" = main ] && echo "$R/block-blast-ai---reinforcement-learning-agent_amd/libbbvec.so" || echo "$R/tools/variants/libbbvec_$n.so"; }
+libof() { local n=${1%%:*}; [ "$n" = main ] && echo "$R/block-blast-ai---reinforcement-learning-agent_amd/libbbvec.so" || echo "$R/build/ab/libbbvec_$n.so"; }
 envof() { local e=${1#*:}; [ "$e" = "$1" ] && echo "" || echo "${e//:/ }"; }
 for v in ${VARIANTS:-main}; do
   env $(envof $v) BBVEC_LIB=$(libof $v) timeout -k 10 600 python -u -m pytest tests/test_gpu_full_parity.py tests/test_gpu_rollout.py \
@@ -18,6 +18,10 @@ for v in ${VARIANTS:-main}; do
     -k "${PK:-rollout_matches or long_horizon or many_workgroups or lemire}" > gpurun_out/${TAG}_pytest_$v.log 2>&1
   rc=$?; echo "$v parity rc=$rc $(tail -1 gpurun_out/${TAG}_pytest_$v.log)"
   [ $rc -eq 0 ] || { tail -30 gpurun_out/${TAG}_pytest_$v.log; exit $rc; }
+done
+for d in ${DIAG:-}; do  # diagnostic builds (BB_ASYNC_DIAG=1): per-wave counters (tools/diag_async.py)
+  BBVEC_LIB=$R/build/ab/libbbvec_$d.so timeout -k 10 120 python3 tools/diag_async.py > gpurun_out/${TAG}_diag_$d.json 2> gpurun_out/${TAG}_diag_$d.err || { tail -5 gpurun_out/${TAG}_diag_$d.err; exit 1; }
+  python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_diag_$d.json'))[-1];print('$d', {k: d[k] for k in ('env_iters_per_step','env_iters_max','env_wave_cyc_mean','env_wave_cyc_max','env_wave_cyc_by_index','slowest_index_share','wg_cyc_mean_of_max','cyc_per_call','envs_per_call')})"
 done
 for r in $(seq 1 ${REPS:-2}); do
   for v in ${VARIANTS:-main}; do
