@@ -225,7 +225,8 @@ def dp_update_leg(dev, rank: int, world: int, steps: int, warmup: int, bf16: boo
     """Per-rank PPO optimizer steps of 2,048 samples (train_minibatch: HIP-graph-replayed forward, fused loss,
     backward, gradient all-reduce over the process group -- RCCL on GPUs -- then clip + Adam), timed between
     barriers (max over ranks), and the same step with no collective (a local agent, world forced to 1): the
-    difference is the all-reduce's exposed time per step.  Plus the full-buffer all-reduce alone."""
+    difference is the all-reduce's exposed time plus the data-parallel step's own extras.  Plus the full-buffer
+    all-reduce alone."""
     import torch
     import torch.distributed as dist
 
@@ -291,7 +292,9 @@ def dp_update_leg(dev, rank: int, world: int, steps: int, warmup: int, bf16: boo
         "backend": dist.get_backend(), "rccl_world_size": dist.get_world_size(),
         "steps": steps, "warmup": warmup,
         "step_ms": round(dp_ms, 4), "local_step_ms": round(local_ms, 4),
-        "exposed_allreduce_ms": round(dp_ms - local_ms, 4),
+        # the collective's exposed time plus the data-parallel step's own extras (the flat gradient buffer's
+        # zero fill and views, the two backward segments, the average) over the single-rank step
+        "dp_minus_local_ms": round(dp_ms - local_ms, 4),
         "allreduce_alone_ms": round(ar_ms, 4), "grad_floats": int(flat.numel()),
         "grad_bytes": int(flat.numel() * 4),
         "allreduce_busbw_gbs": round(2 * (world - 1) / world * flat.numel() * 4 / (ar_ms * 1e-3) / 1e9, 2),
