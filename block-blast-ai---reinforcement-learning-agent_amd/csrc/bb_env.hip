@@ -912,12 +912,6 @@ __global__ void __launch_bounds__(kStepRollBlock, 1) step_fused_kernel(EnvDev e,
 // search waves: the quota pass schedule (gen_hands_quota, bb_solver.h); 0: gen_hands_multi's packed passes
 #define BB_SEARCH_QUOTA 1
 #endif
-#ifndef BB_ASYNC_WINDOW
-// an env moves only while it is fewer than this many steps ahead of the slowest unfinished env of its wave (0: no
-// bound).  Bounds the [step][N] output rows a wave has open at once, so that more of each row's 128-byte lines are
-// complete in L2 before they are written back (unbounded: ~4x the stored output bytes in HBM writes)
-#define BB_ASYNC_WINDOW 0
-#endif
 #ifndef BB_ASYNC_PHILOX_EARLY
 #define BB_ASYNC_PHILOX_EARLY 0  // the policy uniform computed at the top of every iteration (every lane)
 #endif
@@ -1136,14 +1130,7 @@ __global__ void __launch_bounds__(kABlock, 1) rollout_async_kernel(EnvDev e, con
 #endif
     // 1. the move of every ready env and attempt 1's draws when it used the last slot
     //    (block_blast_env.py:237-245, engine.py:326-437)
-#if BB_ASYNC_WINDOW
-    // the slowest unfinished env of the wave (finished lanes read as ~0u and do not count)
-    const uint32_t lo_st = ~(uint32_t)__builtin_amdgcn_readlane(
-        (int)wave_incl_max(~(live && st < T ? (uint32_t)st : 0xFFFFFFFFu)), 63);
-    const bool mv = live && ph == 0 && st < T && (uint32_t)st < lo_st + (uint32_t)BB_ASYNC_WINDOW;
-#else
     const bool mv = live && ph == 0 && st < T;
-#endif
 #if BB_ASYNC_PHILOX_EARLY
     // this step's policy uniform depends only on the env's step counter: its ten dependent Philox rounds
     // overlap the move's LDS round trips (one lane per env: no copy to share it with)

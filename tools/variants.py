@@ -29,11 +29,6 @@ VARIANTS = {
     "an4": ["-DBB_ADAM_NORM_CPB=4"],
     # round 6: the last-arriver hand-offs' arrive add relaxed (the round-5 form) instead of acq_rel
     "hrx": ["-DBB_HANDOFF_ORDER=__ATOMIC_RELAXED"],
-    # round 6: env waves' step window (the output rows open at once) for the write amplification
-    "aw12": ["-DBB_ASYNC_WINDOW=12"],
-    "aw16": ["-DBB_ASYNC_WINDOW=16"],
-    "aw24": ["-DBB_ASYNC_WINDOW=24"],
-    "aw32": ["-DBB_ASYNC_WINDOW=32"],
     # round 5: search waves' pass schedule -- 0: gen_hands_multi's packed passes (round 4); quota per attempt
     # in a round's first pass (shipped 4) and later passes (shipped 64)
     "mq0": ["-DBB_SEARCH_QUOTA=0"],
