@@ -1101,25 +1101,6 @@ extern "C" int bb_dropout_forward(void* d_y, int64_t n, float p, int64_t* d_rng,
   return BB_OK;
 }
 
-extern "C" int64_t bb_linear_relu_workspace_bytes(int32_t M, int32_t N, int32_t K) {
-  return linear_relu_workspace_bytes(M, N, K);
-}
-
-extern "C" int bb_linear_relu_forward(const void* d_x, int64_t ldx, const void* d_w, const void* d_bias, int32_t M,
-                                      int32_t N, int32_t K, float p, int64_t* d_rng, void* d_y, float* d_ws,
-                                      void* stream) {
-  if (!d_x || !d_w || !d_y || !d_ws) return fail(nullptr, BB_ERR_ARG, "bb_linear_relu_forward: NULL argument");
-  if (linear_relu_workspace_bytes(M, N, K) < 0)
-    return fail(nullptr, BB_ERR_ARG, "bb_linear_relu_forward: M, N multiples of 128 and K of 64 required");
-  if (p != 0.f && (!(p > 0.f && p < 1.f) || !d_rng))
-    return fail(nullptr, BB_ERR_ARG, "bb_linear_relu_forward: p must be 0, or in (0, 1) with d_rng");
-  hipError_t st = launch_linear_relu(d_x, ldx, d_w, d_bias, M, N, K, p, d_rng, d_y, d_ws, (hipStream_t)stream);
-  if (st == hipErrorInvalidValue)
-    return fail(nullptr, BB_ERR_ARG, "bb_linear_relu_forward: ldx >= K, a multiple of 8; 16-byte aligned pointers");
-  if (st != hipSuccess) return hip_fail(nullptr, st, "bb_linear_relu_forward");
-  return BB_OK;
-}
-
 extern "C" int bb_linear_bgrad2(const void* d_dy, const void* d_dy2, int32_t split, const void* d_yd, int32_t rows,
                                 int32_t cols, float scale, void* d_g, void* d_db, float* d_ws, uint32_t* d_cnt,
                                 void* stream) {

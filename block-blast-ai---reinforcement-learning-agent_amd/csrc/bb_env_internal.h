@@ -190,9 +190,6 @@ hipError_t launch_cast_multi(int count, int dir, const void* const* src, void* c
 // bf16 Linear tails (bb_optim.hip): in-place dropout with a self-advancing device generator word, and the
 // masked-scale + ReLU-mask + bias-gradient pass of the backward
 hipError_t launch_dropout_fwd(void* y, int64_t n, float p, int64_t* rng, hipStream_t s);
-int64_t linear_relu_workspace_bytes(int M, int N, int K);
-hipError_t launch_linear_relu(const void* x, int64_t ldx, const void* w, const void* bias, int M, int N, int K,
-                              float p, int64_t* rng, void* y, float* ws, hipStream_t s);
 int64_t linear_bgrad_workspace_bytes(int rows, int cols);
 int linear_bgrad_counters(int cols);
 hipError_t launch_linear_bgrad(const void* dy, const void* yd, int rows, int cols, float scale, void* g, void* db,

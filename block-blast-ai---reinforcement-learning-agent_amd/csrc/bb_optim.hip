@@ -822,203 +822,6 @@ __global__ void __launch_bounds__(256) linear_n1_bwd_kernel(const uint16_t* __re
   }
 }
 
-// ---------------------------------------------------------------- the first FC layer's forward
-// y = dropout(relu(x w^T + b)) for a bf16 nn.Linear with a long reduction (network.py:94-103: fc_encoder's
-// Linear(8192, 512) -> ReLU -> Dropout(0.1) under autocast).  hipBLASLt runs it on 64 x 64 tiles over the whole
-// K = 8,192 (256 workgroups re-reading both operands from L2 for every tile: 151 MB fetched for 42 MB of
-// operands, ~23% of the MFMA peak), then the dropout is a second pass.  Here:
-//   linear_tn_splitk_kernel : 128 x 128 output tiles, 4 waves of 64 x 64 (mfma_f32_16x16x32_bf16, 4 x 4 tiles
-//                             each), K split `splits` ways so the grid covers the chip; each K chunk streams
-//                             through a 3-slot LDS ring of 64-deep stages (x rows and w rows, both K-contiguous:
-//                             the MFMA A / B fragments are 16-byte row reads), copied by LDS-DMA two stages ahead
-//                             with counted vmcnt waits; 16-byte chunk c of an LDS row lives at c ^ (row & 7)
-//                             (ds_read_b128's lane groups then hit 16 distinct bank quads).  f32 partials [S][M][N].
-//                             Workgroup b -> tile: blocks b, b + 8, ... share an XCD (MI355X_MICROARCH.md), so
-//                             each XCD takes a run of consecutive tiles (n fastest, then m, then the K split):
-//                             its workgroups share x rows and one K chunk of w in that XCD's L2.
-//   linear_splitk_relu_kernel: adds the S partials in split order (deterministic), + bias, ReLU, rounds to bf16,
-//                             then nn.Dropout exactly as dropout_fwd_kernel (the same Philox draw per element of
-//                             y, the same generator word, advanced by the last workgroup), 8 outputs per thread.
-typedef short bf16x8_t __attribute__((ext_vector_type(8)));
-constexpr int kLtBM = 128, kLtBN = 128, kLtBK = 64, kLtRing = 3;
-constexpr int kLtSlot = (kLtBM + kLtBN) * kLtBK * 2;  // bytes per ring slot: 32 KB
-constexpr int kLtCopies = kLtSlot / 1024 / 4;         // 1-KB LDS-DMA copies per wave per stage (8)
-
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else in this kernel keeps it live
-// global -> LDS copy of one 16-byte chunk per lane (lane L lands at lds_base + 16 L), issued from inline asm
-// so the compiler inserts no vmcnt(0) before the LDS reads of other ring slots (the loop waits counted)
-__device__ __forceinline__ void lt_glds16(const void* g, uint8_t* lds_base) {
-  const uint32_t l = (uint32_t)(size_t)((__attribute__((address_space(3))) uint8_t*)lds_base);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
-}
-#pragma clang diagnostic pop
-#define LT_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (7 << 4) | (15 << 8) | (((n) >> 4) << 14))
-
-__device__ __forceinline__ void lt_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-__global__ void __launch_bounds__(256, 1) linear_tn_splitk_kernel(const uint16_t* __restrict__ x, int ldx,
-                                                                  const uint16_t* __restrict__ w, int M, int N, int K,
-                                                                  int splits, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) uint8_t sm[kLtRing * kLtSlot];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tn = N / kLtBN, tm = M / kLtBM;
-  const int G = tn * tm * splits;
-  const int L = blockIdx.x;
-  const int q = (G % 8 == 0) ? (L & 7) * (G >> 3) + (L >> 3) : L;
-  const int nt = q % tn, rest = q / tn, mt = rest % tm, kz = rest / tm;
-  const int m0 = mt * kLtBM, n0 = nt * kLtBN;
-  const int kch = K / splits, kbeg = kz * kch, NS = kch / kLtBK;
-  // stage s -> ring slot s % kLtRing: 32 copies of 1 KB (0-15 the x tile, 16-31 the w tile), 8 per wave; copy c
-  // chunk e = 64 (c & 15) + lane: row e >> 3, physical chunk e & 7 = logical chunk (e & 7) ^ (row & 7)
-  auto stage = [&](int st) {
-    uint8_t* sb = sm + (st % kLtRing) * kLtSlot;
-    const int k0 = kbeg + st * kLtBK;
-#pragma unroll
-    for (int cq = 0; cq < kLtCopies; ++cq) {
-      const int c = wid * kLtCopies + cq;
-      const int e = (c & 15) * 64 + lane, row = e >> 3, lc = (e & 7) ^ (row & 7);
-      const uint16_t* src = c < 16 ? x + (size_t)(m0 + row) * ldx + k0 + lc * 8 : w + (size_t)(n0 + row) * K + k0 + lc * 8;
-      lt_glds16(src, sb + c * 1024);
-    }
-  };
-#pragma unroll
-  for (int st = 0; st < kLtRing - 1; ++st)
-    if (st < NS) stage(st);
-  if (NS >= 2) LT_WAIT_VM(kLtCopies);  // stage 0 landed (this wave's copies; the others' through the barrier)
-  else LT_WAIT_VM(0);
-  lt_barrier();
-
-  const int r16 = lane & 15, hq = lane >> 4, key = r16 & 7;  // every fragment row is 16-aligned + r16
-  const int wm = wid >> 1, wn = wid & 1;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int arow = (64 * wm + r16) * (kLtBK * 2), brow = kLtBM * kLtBK * 2 + (64 * wn + r16) * (kLtBK * 2);
-#pragma unroll 1
-  for (int st = 0; st < NS; ++st) {
-    if (st + kLtRing - 1 < NS) stage(st + kLtRing - 1);  // its slot was last read in stage st - 1, before the barrier
-    const uint8_t* sb = sm + (st % kLtRing) * kLtSlot;
-    bf16x8_t af[2][4], bfv[2][4];
-    auto load = [&](int kk, int set) {
-      const int ch = ((4 * kk + hq) ^ key) << 4;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[set][i] = *reinterpret_cast<const bf16x8_t*>(sb + arow + i * 16 * kLtBK * 2 + ch);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfv[set][j] = *reinterpret_cast<const bf16x8_t*>(sb + brow + j * 16 * kLtBK * 2 + ch);
-    };
-    load(0, 0);
-#pragma unroll
-    for (int kk = 0; kk < kLtBK / 32; ++kk) {
-      if (kk + 1 < kLtBK / 32) load(kk + 1, (kk + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][i], bfv[kk & 1][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // stage st + 1 must have landed: of this wave's copies, only those of stage st + 2 (if issued) may be out
-    if (st + 2 < NS) LT_WAIT_VM(kLtCopies);
-    else LT_WAIT_VM(0);
-    lt_barrier();
-  }
-  // lane holds D[m = 16 i + 4 hq + e][n = 16 j + r16] of its wave's 64 x 64 tile
-  float* out = part + (size_t)kz * M * N;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = m0 + 64 * wm + 16 * i + 4 * hq + e;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) out[(size_t)m * N + n0 + 64 * wn + 16 * j + r16] = acc[i][j][e];
-    }
-}
-
-__global__ void __launch_bounds__(256) linear_splitk_relu_kernel(const float* __restrict__ part, int64_t MN, int N,
-                                                                 int splits, const uint16_t* __restrict__ bias,
-                                                                 uint16_t* __restrict__ y, int drop,
-                                                                 uint32_t thresh, float scale, int64_t* rng) {
-  uint32_t k0 = 0, k1 = 0, o0 = 0, o1 = 0;
-  if (drop) {
-    const uint64_t seed = (uint64_t)rng[0], off = (uint64_t)rng[1];
-    k0 = (uint32_t)seed;
-    k1 = (uint32_t)(seed >> 32);
-    o0 = (uint32_t)off;
-    o1 = (uint32_t)(off >> 32);
-  }
-  const int64_t stride = (int64_t)gridDim.x * 256 * 8;
-  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < MN; i += stride) {
-    float a[8];
-    {
-      const float4 p0 = *reinterpret_cast<const float4*>(part + i), p1 = *reinterpret_cast<const float4*>(part + i + 4);
-      a[0] = p0.x; a[1] = p0.y; a[2] = p0.z; a[3] = p0.w; a[4] = p1.x; a[5] = p1.y; a[6] = p1.z; a[7] = p1.w;
-    }
-    for (int sp = 1; sp < splits; ++sp) {  // split order
-      const float* ps = part + (size_t)sp * MN + i;
-      const float4 p0 = *reinterpret_cast<const float4*>(ps), p1 = *reinterpret_cast<const float4*>(ps + 4);
-      a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w; a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
-    }
-    const int n = (int)(i % N);
-    uint32_t bw[4] = {0u, 0u, 0u, 0u};
-    if (bias) {
-      const uint4 bv = *reinterpret_cast<const uint4*>(bias + n);
-      bw[0] = bv.x; bw[1] = bv.y; bw[2] = bv.z; bw[3] = bv.w;
-    }
-    uint32_t r[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (drop) {
-      const uint64_t qq = (uint64_t)i >> 2;
-      const Philox4 pa = philox4x32_10((uint32_t)qq, (uint32_t)(qq >> 32), o0, o1, k0, k1);
-      const Philox4 pb = philox4x32_10((uint32_t)(qq + 1), (uint32_t)((qq + 1) >> 32), o0, o1, k0, k1);
-      r[0] = pa.v[0]; r[1] = pa.v[1]; r[2] = pa.v[2]; r[3] = pa.v[3];
-      r[4] = pb.v[0]; r[5] = pb.v[1]; r[6] = pb.v[2]; r[7] = pb.v[3];
-    }
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint16_t h[2];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int j = 2 * k + hh;
-        const float bj = bias ? bf2f((uint16_t)(hh ? (bw[k] >> 16) : (bw[k] & 0xffffu))) : 0.f;
-        const uint16_t v = f2bf_rne(fmaxf(a[j] + bj, 0.f));  // the GEMM epilogue: acc + bias, ReLU, one rounding
-        h[hh] = drop ? (r[j] >= thresh ? f2bf_rne(bf2f(v) * scale) : (uint16_t)0) : v;
-      }
-      o[k] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-    }
-    *reinterpret_cast<uint4*>(y + i) = make_uint4(o[0], o[1], o[2], o[3]);
-  }
-  if (!drop) return;
-  __syncthreads();  // every thread's (seed, offset) load has returned before the block counts itself
-  if (threadIdx.x == 0) {
-    const uint64_t prev = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(rng + 2), 1ull,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (uint64_t)gridDim.x - 1) {  // the last block: every block has read the offset
-      const uint64_t off = (uint64_t)rng[1];
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(rng + 1), (unsigned long long)(off + 1),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(rng + 2), 0ull, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// K splits of the forward GEMM: enough workgroups to cover the chip (~256), each K chunk a multiple of 64
-int lt_splits(int M, int N, int K) {
-  const int tiles = (M / kLtBM) * (N / kLtBN);
-  int s = 1;
-  while (s < 8 && tiles * s * 2 <= 256 && K % (kLtBK * s * 2) == 0) s *= 2;
-  return s;
-}
-
 int build_adam_table(AdamTable& tab, int count, float* const* p, float* const* g, float* const* m, float* const* v,
                      float* const* step, const int64_t* n) {
   if (count <= 0 || count > kOptMaxTensors) return -1;
@@ -1105,40 +908,6 @@ hipError_t launch_dropout_fwd(void* y, int64_t n, float p, int64_t* rng, hipStre
   if (blocks > kDropMaxBlocks) blocks = kDropMaxBlocks;  // grid-stride: few arrivals on the generator word
   hipLaunchKernelGGL(dropout_fwd_kernel, dim3((unsigned)blocks), dim3(kDropThreads), 0, s, (uint16_t*)y, n,
                      thresh, scale, rng);
-  return hipGetLastError();
-}
-
-int64_t linear_relu_workspace_bytes(int M, int N, int K) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % kLtBM || N % kLtBN || K % kLtBK) return -1;
-  return (int64_t)lt_splits(M, N, K) * M * N * (int64_t)sizeof(float);
-}
-
-hipError_t launch_linear_relu(const void* x, int64_t ldx, const void* w, const void* bias, int M, int N, int K,
-                              float p, int64_t* rng, void* y, float* ws, hipStream_t s) {
-  if (!x || !w || !y || !ws || M <= 0 || N <= 0 || K <= 0 || M % kLtBM || N % kLtBN || K % kLtBK || ldx < K ||
-      ldx % 8 || ldx > (int64_t)1 << 30 ||
-      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y) |
-        reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(ws)) & 15) ||
-      (p != 0.f && (!(p > 0.f && p < 1.f) || !rng)))
-    return hipErrorInvalidValue;
-  const int splits = lt_splits(M, N, K);
-  const int grid = (M / kLtBM) * (N / kLtBN) * splits;
-  hipLaunchKernelGGL(linear_tn_splitk_kernel, dim3((unsigned)grid), dim3(256), 0, s, (const uint16_t*)x, (int)ldx,
-                     (const uint16_t*)w, M, N, K, splits, ws);
-  uint32_t thresh = 0u;
-  float scale = 1.f;
-  if (p != 0.f) {  // as launch_dropout_fwd
-    const float keep = (float)(1.0 - (double)p);
-    scale = (float)(1.0 / (double)keep);
-    const double t = (double)p * 4294967296.0;
-    thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
-  }
-  const int64_t MN = (int64_t)M * N;
-  int64_t blocks = (MN / 8 + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(linear_splitk_relu_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)ws, MN, N,
-                     splits, (const uint16_t*)bias, (uint16_t*)y, p != 0.f ? 1 : 0, thresh, scale,
-                     p != 0.f ? rng : nullptr);
   return hipGetLastError();
 }
 

@@ -1055,35 +1055,6 @@ def linear_wgrad(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return g.t().mm(x)
 
 
-# the first FC layer's forward on bb_linear_relu_forward (split-K MFMA GEMM + one epilogue pass: bias, ReLU, dropout)
-# instead of hipBLASLt's GEMM + bb_dropout_forward (0: those, for A/B); only for long reductions (K >= FC_GEMM_MIN_K)
-FC_GEMM = os.environ.get("BB_FC_GEMM", "1") != "0"
-FC_GEMM_MIN_K = 4096
-FC_GEMM_MAX_M = 16384  # the update's minibatches; the rollout's 65,536+ rows stay on hipBLASLt (no K split to pay for)
-
-
-def _fc_gemm_ok(x: torch.Tensor, weight: torch.Tensor, bias) -> bool:
-    m, k = x.shape
-    n = weight.shape[0]
-    return (FC_GEMM and _rows_ok(x) and _bgrad_ok(weight) and weight.shape[1] == k and k >= FC_GEMM_MIN_K
-            and 0 < m <= FC_GEMM_MAX_M and m % 128 == 0 and n % 128 == 0 and k % 64 == 0
-            and weight.data_ptr() % 16 == 0
-            and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.data_ptr() % 16 == 0)))
-
-
-def linear_relu_forward(x: torch.Tensor, weight: torch.Tensor, bias, p: float = 0.0, rng=None) -> torch.Tensor:
-    """dropout(relu(x w^T + b)) on bb_linear_relu_forward (bf16; _fc_gemm_ok shapes)."""
-    m, k = x.shape
-    n = weight.shape[0]
-    lib = L.load()
-    y = torch.empty((m, n), dtype=torch.bfloat16, device=x.device)
-    ws = torch.empty((lib.bb_linear_relu_workspace_bytes(m, n, k) + 3) // 4, dtype=torch.float32, device=x.device)
-    L.check(lib.bb_linear_relu_forward(_p(x), x.stride(0), _p(weight), _p(bias), m, n, k, float(p),
-                                       _p(rng) if p > 0.0 else None, _p(y), _p(ws), _s(x.device)),
-            "bb_linear_relu_forward")
-    return y
-
-
 class LinearReLUFunction(torch.autograd.Function):
     """dropout(relu(F.linear(x, w, b)), p) for 2-D x: the ReLU in hipBLASLt's GEMM epilogue
     (torch._addmm_activation), then -- p > 0, nn.Dropout in training -- bb_dropout_forward in place (its
@@ -1093,15 +1064,8 @@ class LinearReLUFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, p: float = 0.0, rng: Optional[torch.Tensor] = None):
-        scale = 1.0
-        if _fc_gemm_ok(x, weight, bias) and (p == 0.0 or rng is not None):
-            y = linear_relu_forward(x, weight, bias, p, rng)
-            if p > 0.0:
-                scale = 1.0 / struct.unpack("f", struct.pack("f", 1.0 - p))[0]
-            ctx.save_for_backward(x, weight, y)
-            ctx.scale = scale
-            return y
         y = torch._addmm_activation(bias, x, weight.t())
+        scale = 1.0
         if p > 0.0:
             if rng is None or y.numel() % 8 or not _bgrad_ok(y):
                 raise L.BBNativeError("LinearReLUFunction: dropout needs a bf16 output of 8k elements and rng")

@@ -60,7 +60,7 @@ class Info(C.Structure):
     ]
 
 
-ABI_VERSION = 9  # include/bbvec.h BB_ABI_VERSION
+ABI_VERSION = 8  # include/bbvec.h BB_ABI_VERSION
 INFO_BYTES = C.sizeof(Info)  # 56, matches sizeof(bb_info)
 
 
@@ -182,8 +182,6 @@ SIGNATURES = {
                                     _P, _P, _P]),
     "bb_cast_multi": (C.c_int, [_I32, _I32, _P, _P, _P, _P, _P, _P]),
     "bb_dropout_forward": (C.c_int, [_P, C.c_int64, _F, _P, _P]),
-    "bb_linear_relu_workspace_bytes": (C.c_int64, [_I32, _I32, _I32]),
-    "bb_linear_relu_forward": (C.c_int, [_P, C.c_int64, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P]),
     "bb_conv_in_wgrad_workspace_bytes": (C.c_int64, [_I32]),
     "bb_conv_in_forward": (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     "bb_conv_in_wgrad": (C.c_int, [_P, _I32, _P, _I32, _P, _I32, _P, _P]),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 9  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
+#define BB_ABI_VERSION 8  /* 2: bb_step_out.final_score / final_moves; 3: bb_sync, BB_ERR_DEVICE;
                               4: bb_conv_in_* and bb_relu_bias_grad* removed;
                               5: bb_conv3x3_forward_stats / _stats_parts and bb_bn_forward_parts removed;
                               6: bb_build_id; bb_obs / bb_snapshot report BB_ERR_DEVICE;
@@ -44,8 +44,7 @@ extern "C" {
                                  bb_conv3x3_wgrad_partial / _reduce / _chunks, bb_bn_backward_red,
                                  bb_conv_in_forward_prep, bb_linear_bgrad2, bb_conv3x3_forward_stats,
                                  bb_conv3x3_stats_blocks, bb_bn_forward_part, bb_conv3x3_forward_bstats,
-                                 bb_bn_backward_part;
-                              9: bb_linear_relu_forward / _workspace_bytes; the Adam guard word */
+                                 bb_bn_backward_part */
 
 #define BB_OK 0
 #define BB_ERR_ARG (-1)
@@ -544,17 +543,6 @@ int bb_cast_multi(int32_t num_tensors, int32_t dir, const void* const* h_src, vo
  * and are zero again after each (the launch re-arms them) -- one counter block per stream: launches that run
  * concurrently must not share one. */
 int bb_dropout_forward(void* d_y, int64_t n, float p, int64_t* d_rng, void* stream);
-/* bb_linear_relu_forward (ABI 9): y = dropout(relu(x w^T + b)) for a bf16 Linear with a long reduction (the first
- * fc_encoder layer, network.py:94-103, under autocast) in two launches instead of hipBLASLt's GEMM + the dropout
- * pass.  x bf16 [M][K] with row stride ldx (>= K, a multiple of 8), w bf16 [N][K] (nn.Linear.weight), b bf16 [N]
- * or NULL, y bf16 [M][N]; M and N multiples of 128, K of 64, 16-byte aligned pointers.  f32 sums: K split over
- * workgroups into f32 partials in d_ws (bb_linear_relu_workspace_bytes(M, N, K) bytes), added in split order
- * (deterministic), + b, ReLU, rounded to bf16 once -- the GEMM epilogue's arithmetic.  p = 0: no dropout; p in
- * (0, 1): bb_dropout_forward's mask and scale on that output, from the same generator word d_rng (advanced by
- * one, so the same draws as a bb_dropout_forward launch in its place). */
-int64_t bb_linear_relu_workspace_bytes(int32_t M, int32_t N, int32_t K);
-int bb_linear_relu_forward(const void* d_x, int64_t ldx, const void* d_w, const void* d_bias, int32_t M, int32_t N,
-                           int32_t K, float p, int64_t* d_rng, void* d_y, float* d_ws, void* stream);
 
 /* The CNN's input layer, conv 4 -> 64 3x3 pad 1 over 8x8 boards (network.py:75-87, the first nn.Conv2d, without
  * its bias: the BatchNorm after it adds that) under bf16 autocast, not part of the env boundary.  x: N boards

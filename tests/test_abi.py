@@ -24,7 +24,7 @@ def test_header_and_binding_agree():
 def test_library_exports_every_symbol(lib):
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.bb_abi_version() == L.ABI_VERSION == 9
+    assert lib.bb_abi_version() == L.ABI_VERSION == 8
 
 
 def test_build_id_is_these_sources(lib):

@@ -186,49 +186,6 @@ def test_linear_relu_dropout_function(cuda):
     assert bool(((b.grad.double() - exact).abs() <= 2.0 ** -8 * exact.abs() + 1e-5 * g.double().abs().sum(0)).all())
 
 
-@pytest.mark.parametrize("m,n,k,bias", [(2048, 512, 8192, True), (256, 128, 4096, False), (1024, 256, 8192, True)])
-def test_linear_relu_forward_matches_fp64(cuda, m, n, k, bias):
-    """bb_linear_relu_forward (split-K MFMA GEMM, then + b, ReLU, one bf16 rounding): within one bf16 rounding of
-    the fp64 relu(x w^T + b) of the same bf16 operands, deterministic run to run; a column slice of a wider x too."""
-    from runtime import kernels as K
-
-    g0 = torch.Generator(device=cuda).manual_seed(11)
-    xw = _bf(torch.randn((m, k + 64), device=cuda, generator=g0))
-    x = xw[:, :k]  # row stride k + 64
-    w = _bf(torch.randn((n, k), device=cuda, generator=g0) * k ** -0.5)
-    b = _bf(torch.randn(n, device=cuda, generator=g0) * 0.1) if bias else None
-    y = K.linear_relu_forward(x, w, b)
-    ref = x.double().mm(w.double().t()) + (b.double() if bias else 0.0)
-    ref = ref.clamp_min(0.0)
-    err = (y.double() - ref).abs()
-    assert bool((err <= 2.0 ** -8 * ref.abs() + 1e-6).all()), float(err.max())
-    assert torch.equal(y, K.linear_relu_forward(x, w, b))
-    assert K._fc_gemm_ok(x, w, b)
-
-
-def test_linear_relu_forward_dropout_matches_two_pass(cuda):
-    """With dropout: the mask and scale of bb_dropout_forward drawn from the same generator word (the same elements
-    kept, kept values bf16(y * scale) of this kernel's own y), and the word advanced by one."""
-    import struct
-
-    from runtime import kernels as K
-
-    g0 = torch.Generator(device=cuda).manual_seed(12)
-    x = _bf(torch.randn((2048, 8192), device=cuda, generator=g0))
-    w = _bf(torch.randn((512, 8192), device=cuda, generator=g0) * 8192 ** -0.5)
-    b = _bf(torch.randn(512, device=cuda, generator=g0) * 0.1)
-    plain = K.linear_relu_forward(x, w, b)
-    rng = torch.tensor([4242, 3, 0, 0], dtype=torch.int64, device=cuda)
-    y = K.linear_relu_forward(x, w, b, 0.1, rng)
-    assert rng.tolist() == [4242, 4, 0, 0]
-    two = plain.clone()
-    _dropout(two, 0.1, torch.tensor([4242, 3, 0, 0], dtype=torch.int64, device=cuda))
-    assert torch.equal(y, two)
-    scale = 1.0 / struct.unpack("f", struct.pack("f", 0.9))[0]
-    kept = y != 0
-    assert torch.equal(y[kept], _bf(plain.float() * scale)[kept])
-
-
 def test_network_linear_tail_equals_torch_tails(cuda, monkeypatch):
     """bf16 raw() forward + backward with dropout at 0: the fused tails (bb_linear_bgrad, LinearBiasFunction)
     give torch's logits and values bit for bit and its Linear gradients within bf16 rounding."""
@@ -245,7 +202,6 @@ def test_network_linear_tail_equals_torch_tails(cuda, monkeypatch):
     state0 = {k: v.clone() for k, v in net.state_dict().items()}
     res = {}
     monkeypatch.setattr(N, "HEADS_FUSED", False)  # the joint heads GEMM is test_heads_function_*'s
-    monkeypatch.setattr(K, "FC_GEMM", False)  # the first FC layer's own GEMM: test_linear_relu_forward_*'s
     for tail in (True, False):
         monkeypatch.setattr(K, "LINEAR_TAIL", tail)
         net.load_state_dict(state0)
