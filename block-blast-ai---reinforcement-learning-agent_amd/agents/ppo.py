@@ -30,6 +30,7 @@ import torch.nn.functional as F
 
 from models.network import BlockBlastNetwork, masked_entropy
 from runtime import kernels as K
+from runtime import lib as L
 
 from .base import BaseAgent
 
@@ -334,6 +335,7 @@ class PPOAgent(BaseAgent):
         # bb_adam_clip_step scratch per parameter-size set; never dropped, since captured optimizer
         # steps hold the workspace's address
         self._adam_ws: Dict[Tuple[int, ...], torch.Tensor] = {}
+        self._adam_tables: Dict[Tuple[int, ...], Any] = {}  # key -> (params, gradient addresses) last stepped
         # update(): keep every minibatch's 6 statistics (device tensors) in minibatch_stats (parity tests)
         self.record_minibatch_stats = False
         self.minibatch_stats: List[torch.Tensor] = []
@@ -652,6 +654,9 @@ class PPOAgent(BaseAgent):
         ws = self._adam_ws.get(key)
         if ws is None:
             ws = self._adam_ws[key] = K.adam_clip_workspace(list(key), self.device)
+        # for the guard's report: the parameters and gradient addresses this table (and any graph it is captured
+        # into) reads
+        self._adam_tables[key] = (params, tuple(p.grad.data_ptr() for p in params))
         b1, b2 = grp["betas"]
         K.adam_clip_step(params, [p.grad for p in params], [opt.state[p]["exp_avg"] for p in params],
                          [opt.state[p]["exp_avg_sq"] for p in params], [opt.state[p]["step"] for p in params],
@@ -663,9 +668,23 @@ class PPOAgent(BaseAgent):
         check (bb_adam_clip_step's guard word, csrc/bb_optim.hip adam_finalize_kernel), naming the parameter."""
         if not self._adam_ws:
             return
-        names = [n for n, p in self.network.named_parameters() if p.requires_grad]
+        pname = {id(p): n for n, p in self.network.named_parameters()}
         for key, ws in self._adam_ws.items():
-            K.adam_guard_check(ws, key, names if len(names) == len(key) else None)
+            params, ptrs = self._adam_tables.get(key, ((), ()))
+            names = [pname.get(id(p), "?") for p in params] if params else None
+            try:
+                K.adam_guard_check(ws, key, names)
+            except L.BBNativeError as exc:  # what the table read against what .grad holds now
+                info = []
+                for p, ptr, n in zip(params, ptrs, names or []):
+                    g = p.grad
+                    cur = g.data_ptr() if g is not None else 0
+                    fin = bool(torch.isfinite(g).all()) if g is not None else None
+                    nrm = float(g.detach().double().norm()) if g is not None and fin else None
+                    if cur != ptr or not fin or (nrm is not None and nrm > 1e6):
+                        info.append(f"{n}: table grad 0x{ptr:x}, .grad 0x{cur:x}, finite {fin}, norm {nrm}")
+                # (the clip rescaled every .grad in place since the flagged read: a finite norm here says little)
+                raise L.BBNativeError(f"{exc}; {'; '.join(info) if info else 'every .grad is the table one'}")
 
     def _clip_and_step(self) -> None:
         """clip_grad_norm_(max_grad_norm) + Adam.step() (ppo.py:397-401)."""
