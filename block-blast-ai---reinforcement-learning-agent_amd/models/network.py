@@ -103,6 +103,11 @@ def _linear(x: torch.Tensor, lin: nn.Linear, weight: Optional[torch.Tensor] = No
         from runtime.kernels import linear_f32
 
         return linear_f32(x, w, lin.bias)
+    if x.is_cuda:
+        from runtime.kernels import LinearF32Function, linear_f32_train_ok
+
+        if linear_f32_train_ok(x, w, lin.bias):  # the bias gradient as a GEMV (graph-replay safe)
+            return LinearF32Function.apply(x, w, lin.bias)
     return F.linear(x, w, lin.bias)
 
 

@@ -1112,6 +1112,38 @@ class LinearBiasFunction(torch.autograd.Function):
         return dx, dw, db
 
 
+class LinearF32Function(torch.autograd.Function):
+    """F.linear(x, w, b) for 2-D fp32 x in a training forward (no autocast), with the bias gradient as a GEMV
+    (dy^T 1) instead of autograd's dy.sum(0).  torch's sum over the batch runs as a global-memory reduction whose
+    semaphores are zeroed by a hipMemsetAsync before each launch; replayed from PPOAgent's captured optimizer step
+    that reduction sporadically left its output unwritten (a NaN canary in .grad survived the replay, the
+    semaphore counts 16 / 32 sat in its first words) and the Adam guard flagged it -- tools/diag_graph_grad.py:
+    95 of 100 replays flagged with the reduction, 0 of 100 (twice) with the GEMV."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        return torch.addmm(bias, x, weight.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = gy.mm(weight) if ctx.needs_input_grad[0] else None
+        dw = gy.t().mm(x) if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.needs_input_grad[2]:
+            db = gy.t().mv(torch.ones(gy.shape[0], dtype=gy.dtype, device=gy.device))
+        return dx, dw, db
+
+
+def linear_f32_train_ok(x: torch.Tensor, weight: torch.Tensor, bias) -> bool:
+    """LinearF32Function applies: a 2-D fp32 device input, fp32 weight and bias, gradients recorded."""
+    return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and weight.dtype == torch.float32
+            and bias is not None and bias.dtype == torch.float32 and torch.is_grad_enabled()
+            and not torch.is_autocast_enabled("cuda"))
+
+
 class LinearN1Function(torch.autograd.Function):
     """F.linear(x, w, b) for a one-output bf16 Linear (the value head's last layer) on bb_linear_n1_forward /
     _backward: one launch each way instead of torch's bias copy + GEMM and two GEMMs + a reduction."""

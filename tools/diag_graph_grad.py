@@ -65,8 +65,36 @@ def poison(kind):
     gc.collect()
 
 
+class _LinearMV(torch.autograd.Function):
+    """F.linear for 2-D fp32 input whose bias gradient is a GEMV (g^T 1) instead of torch's sum(0) reduction."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        ones = torch.ones(g.shape[0], dtype=g.dtype, device=g.device)
+        return g.mm(w), g.t().mm(x), g.t().mv(ones)
+
+
+def _patch_linear():
+    orig = torch.nn.functional.linear
+
+    def lin(x, w, b=None):
+        if b is not None and x.dim() == 2 and x.is_cuda and x.dtype == torch.float32 and torch.is_grad_enabled():
+            return _LinearMV.apply(x, w, b)
+        return orig(x, w, b)
+
+    torch.nn.functional.linear = lin
+
+
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "graphed"
+    if "mvlinear" in sys.argv[3:]:
+        _patch_linear()
     poison(kind)
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     # lr 0: the parameters never move, so the graphed and eager agents stay comparable step after step
