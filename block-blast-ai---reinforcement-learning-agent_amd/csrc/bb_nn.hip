@@ -420,6 +420,15 @@ __global__ void __launch_bounds__(kBnThreads) bn_finalize_bwd(const double* __re
   o[1] = make_float4(is, mg, mgx, 0.f);
 }
 
+// BB_BN_APPLY_UNROLL chunks of a thread's grid-stride sequence loaded before any is computed (1: one at a time).
+// Measured on the bf16 update step (round 6, tools/gpu_update_ab2.sh, three interleaved repeats per box): 2 within
+// -0.3..0%, 4 +1.7%, 8 +2.5%; BB_BN_APPLY_PT 1 / 2 / 4 / 16 / 32 chunks per thread +23% / +8% / +1% / +1% / +7%.
+// The passes' 4.4 TB/s is not a loads-in-flight limit.
+#ifndef BB_BN_APPLY_UNROLL
+#define BB_BN_APPLY_UNROLL 1
+#endif
+constexpr int kApplyU = BB_BN_APPLY_UNROLL;
+
 // Channel of element j of 16-byte chunk i: NCHW rows are (n, c) with HW / V
 // chunks each (one channel per chunk); NHWC rows are (n, h, w) with C / V
 // chunks of V channels each.  The NHWC grid stride is a multiple of C / V, so
@@ -435,25 +444,37 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_fwd(const void* __restric
   constexpr int NC = NHWC ? V : 1;
   const float4* cf = reinterpret_cast<const float4*>(coef);
   const int64_t g0 = (int64_t)blockIdx.x * kBnThreads + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBnThreads;
   float4 k[NC];
   if (NHWC) {
     const int c0 = (int)(g0 % cpr) * V;
 #pragma unroll
     for (int j = 0; j < NC; ++j) k[j] = cf[(c0 + j) * (kCoef / 4)];
   }
-  for (int64_t i = g0; i < total; i += (int64_t)gridDim.x * kBnThreads) {
-    if (!NHWC) k[0] = cf[(int)((i / cpr) % C) * (kCoef / 4)];
-    float f[V], fr[V];
-    Vec<T>::load(x, i, f);
-    if (res) Vec<T>::load(res, i, fr);
+  for (int64_t i0 = g0; i0 < total; i0 += kApplyU * stride) {
+    float f[kApplyU][V], fr[kApplyU][V];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const float4& q = k[NHWC ? j : 0];  // {pb, mu, sc, sh}
-      float v = (f[j] + q.x - q.y) * q.z + q.w;
-      if (res) v = Vec<T>::round(v) + fr[j];
-      f[j] = relu ? fmaxf(v, 0.f) : v;
+    for (int u = 0; u < kApplyU; ++u) {  // every load in flight before the arithmetic
+      const int64_t i = i0 + u * stride;
+      if (i < total) {
+        Vec<T>::load(x, i, f[u]);
+        if (res) Vec<T>::load(res, i, fr[u]);
+      }
     }
-    Vec<T>::store(y, i, f);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= total) break;
+      if (!NHWC) k[0] = cf[(int)((i / cpr) % C) * (kCoef / 4)];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float4& q = k[NHWC ? j : 0];  // {pb, mu, sc, sh}
+        float v = (f[u][j] + q.x - q.y) * q.z + q.w;
+        if (res) v = Vec<T>::round(v) + fr[u][j];
+        f[u][j] = relu ? fmaxf(v, 0.f) : v;
+      }
+      Vec<T>::store(y, i, f[u]);
+    }
   }
 }
 
@@ -465,6 +486,7 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restric
   constexpr int NC = NHWC ? V : 1;
   const float4* cf = reinterpret_cast<const float4*>(coef);
   const int64_t g0 = (int64_t)blockIdx.x * kBnThreads + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBnThreads;
   float4 k0[NC], k1[NC];
   if (NHWC) {
     const int c0 = (int)(g0 % cpr) * V;
@@ -474,25 +496,36 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_bwd(const void* __restric
       k1[j] = cf[(c0 + j) * (kCoef / 4) + 1];
     }
   }
-  for (int64_t i = g0; i < total; i += (int64_t)gridDim.x * kBnThreads) {
-    if (!NHWC) {
-      const int c = (int)((i / cpr) % C);
-      k0[0] = cf[c * (kCoef / 4)];
-      k1[0] = cf[c * (kCoef / 4) + 1];
-    }
-    float fx[V], fg[V];
-    Vec<T>::load(x, i, fx);
-    Vec<T>::load(dy, i, fg);
+  for (int64_t i0 = g0; i0 < total; i0 += kApplyU * stride) {
+    float fx[kApplyU][V], fg[kApplyU][V];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const float4& a = k0[NHWC ? j : 0];  // {pb, mu, sc, sh}
-      const float4& q = k1[NHWC ? j : 0];  // {is, mg, mgx, -}
-      const float u = fx[j] + a.x;
-      const float g = (relu && (u - a.y) * a.z + a.w <= 0.f) ? 0.f : fg[j];  // the forward's exact ops
-      const float xh = (u - a.y) * q.x;
-      fx[j] = a.z * (g - q.y - xh * q.z);
+    for (int u = 0; u < kApplyU; ++u) {  // every load in flight before the arithmetic
+      const int64_t i = i0 + u * stride;
+      if (i < total) {
+        Vec<T>::load(x, i, fx[u]);
+        Vec<T>::load(dy, i, fg[u]);
+      }
     }
-    Vec<T>::store(dx, i, fx);
+#pragma unroll
+    for (int u = 0; u < kApplyU; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= total) break;
+      if (!NHWC) {
+        const int c = (int)((i / cpr) % C);
+        k0[0] = cf[c * (kCoef / 4)];
+        k1[0] = cf[c * (kCoef / 4) + 1];
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float4& a = k0[NHWC ? j : 0];  // {pb, mu, sc, sh}
+        const float4& q = k1[NHWC ? j : 0];  // {is, mg, mgx, -}
+        const float u_ = fx[u][j] + a.x;
+        const float g = (relu && (u_ - a.y) * a.z + a.w <= 0.f) ? 0.f : fg[u][j];  // the forward's exact ops
+        const float xh = (u_ - a.y) * q.x;
+        fx[u][j] = a.z * (g - q.y - xh * q.z);
+      }
+      Vec<T>::store(dx, i, fx[u]);
+    }
   }
 }
 

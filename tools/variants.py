@@ -25,6 +25,20 @@ VARIANTS = {
     "main": [],
     # BatchNorm finalisation: one wave per channel (round 4) instead of one workgroup
     "fin4": ["-DBB_BN_FIN_CPB=4"],
+    # round 6: BatchNorm apply passes' loads per thread in flight (shipped 1, the round-5 form)
+    "bau1": ["-DBB_BN_APPLY_UNROLL=1"],
+    "bau2": ["-DBB_BN_APPLY_UNROLL=2"],
+    "bau4": ["-DBB_BN_APPLY_UNROLL=4"],
+    "bau8": ["-DBB_BN_APPLY_UNROLL=8"],
+    # chunks per thread of the NHWC apply grids (shipped 8): more, smaller workgroups
+    "bpt4": ["-DBB_BN_APPLY_PT=4"],
+    "bpt16": ["-DBB_BN_APPLY_PT=16"],
+    "bpt16u1": ["-DBB_BN_APPLY_PT=16", "-DBB_BN_APPLY_UNROLL=1"],
+    "bpt16u4": ["-DBB_BN_APPLY_PT=16", "-DBB_BN_APPLY_UNROLL=4"],
+    "bpt32": ["-DBB_BN_APPLY_PT=32"],
+    "bpt2": ["-DBB_BN_APPLY_PT=2"],
+    "bpt2u1": ["-DBB_BN_APPLY_PT=2", "-DBB_BN_APPLY_UNROLL=1"],
+    "bpt1u1": ["-DBB_BN_APPLY_PT=1", "-DBB_BN_APPLY_UNROLL=1"],
     # the gradient-norm pass: four 2,048-element chunks per workgroup (measured slower)
     "an4": ["-DBB_ADAM_NORM_CPB=4"],
     # round 6: the last-arriver hand-offs' arrive add relaxed (the round-5 form) instead of acq_rel
