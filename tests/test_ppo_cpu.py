@@ -159,3 +159,26 @@ def test_data_parallel_grad_allreduce_gloo():
     for r in res:
         assert abs(r[2] - allv.mean()) < 1e-6 and abs(r[3] - allv.std()) < 1e-5
     assert res[0][4] == pytest.approx(res[1][4])  # identical weights after broadcast
+
+
+def test_linear_f32_function_gradients_match_autograd():
+    """runtime.kernels.LinearF32Function (the fp32 training Linear whose bias gradient is a GEMV, dy^T 1, instead
+    of autograd's dy.sum(0)) gives F.linear's output and gradients; the function is device-agnostic, so this runs
+    on CPU tensors (linear_f32_train_ok routes only CUDA inputs to it)."""
+    from runtime.kernels import LinearF32Function, linear_f32_train_ok
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(37, 24, generator=g, dtype=torch.float64).float().requires_grad_(True)
+    w = torch.randn(16, 24, generator=g).requires_grad_(True)
+    b = torch.randn(16, generator=g).requires_grad_(True)
+    dy = torch.randn(37, 16, generator=g)
+    y = LinearF32Function.apply(x, w, b)
+    y.backward(dy)
+    got = (y.detach(), x.grad.clone(), w.grad.clone(), b.grad.clone())
+    for t in (x, w, b):
+        t.grad = None
+    y_ref = torch.nn.functional.linear(x, w, b)
+    y_ref.backward(dy)
+    for a, e in zip(got, (y_ref.detach(), x.grad, w.grad, b.grad)):
+        torch.testing.assert_close(a, e, rtol=1e-5, atol=1e-5)
+    assert not linear_f32_train_ok(x, w, b)  # CPU input: F.linear's own path
