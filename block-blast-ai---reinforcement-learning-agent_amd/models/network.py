@@ -78,6 +78,9 @@ RES_GRAD_FUSED = os.environ.get("BB_RES_GRAD_FUSED", "1") != "0"
 # the update's forward + data gradient on it.
 F32_CONV = os.environ.get("BB_F32_CONV", "1") != "0"
 F32_CONV_GRAD = os.environ.get("BB_F32_CONV_GRAD", "0") == "1"
+# fp32 training Linear layers with the bias gradient as a GEMV (runtime.kernels.LinearF32Function); 0: F.linear,
+# whose batch-sum bias gradient is NOT safe under PPOAgent's graph replay (kept only to measure the cost)
+F32_LINEAR_GEMV = os.environ.get("BB_F32_LINEAR_GEMV", "1") != "0"
 
 
 def _f32_conv_on(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -103,7 +106,7 @@ def _linear(x: torch.Tensor, lin: nn.Linear, weight: Optional[torch.Tensor] = No
         from runtime.kernels import linear_f32
 
         return linear_f32(x, w, lin.bias)
-    if x.is_cuda:
+    if x.is_cuda and F32_LINEAR_GEMV:
         from runtime.kernels import LinearF32Function, linear_f32_train_ok
 
         if linear_f32_train_ok(x, w, lin.bias):  # the bias gradient as a GEMV (graph-replay safe)
