@@ -23,6 +23,13 @@ VARIANTS = {
     # the round-3 compile-time variants measured slower were removed (tools/patches/r03_compile_variants.diff
     # restores them), so their A/B arms cannot be rebuilt from this tree.
     "main": [],
+    # round 6: LLVM machine-scheduler strategy and unroll threshold re-measured on the current kernels (shipped:
+    # max-ilp, 600; round 2 measured them on the round-2 rollout kernel)
+    "siilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    "simaxocc": ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"],
+    "sminreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
+    "u300": ["-mllvm", "-unroll-threshold=300"],
+    "u1200": ["-mllvm", "-unroll-threshold=1200"],
     # BatchNorm finalisation: one wave per channel (round 4) instead of one workgroup
     "fin4": ["-DBB_BN_FIN_CPB=4"],
     # round 6: BatchNorm apply passes' loads per thread in flight (shipped 1, the round-5 form)
