@@ -30,6 +30,9 @@ VARIANTS = {
     "sminreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
     "u300": ["-mllvm", "-unroll-threshold=300"],
     "u1200": ["-mllvm", "-unroll-threshold=1200"],
+    "o2": ["-O2"],
+    "trk": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+    "nocl": ["-mllvm", "-misched-cluster=0"],
     # BatchNorm finalisation: one wave per channel (round 4) instead of one workgroup
     "fin4": ["-DBB_BN_FIN_CPB=4"],
     # round 6: BatchNorm apply passes' loads per thread in flight (shipped 1, the round-5 form)
