@@ -37,6 +37,11 @@ VARIANTS = {
     "fin4": ["-DBB_BN_FIN_CPB=4"],
     # round 6: BatchNorm apply passes' loads per thread in flight (shipped 1, the round-5 form)
     "bau1": ["-DBB_BN_APPLY_UNROLL=1"],
+    # BatchNorm NHWC reductions re-measured on the round-6 step: blocks (shipped 512), backward rows in flight
+    # (shipped 2)
+    "rb256": ["-DBB_BN_RBLOCKS=256"],
+    "rb1024": ["-DBB_BN_RBLOCKS=1024"],
+    "ub4": ["-DBB_BN_UNROLL_BWD=4"],
     "bau2": ["-DBB_BN_APPLY_UNROLL=2"],
     "bau4": ["-DBB_BN_APPLY_UNROLL=4"],
     "bau8": ["-DBB_BN_APPLY_UNROLL=8"],
